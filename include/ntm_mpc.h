@@ -1,0 +1,152 @@
+/*
+ * ntm_mpc.h — C-ABI of the MI355X-native batched LPV-MPC hot path.
+ *
+ * Drop-in boundary for the receding-horizon loop of the MATLAB reference
+ * IsaacSavona/MPC-NTM-Control (NTM_MPC_Sim.m:93-131).  The reference has no
+ * FFI of its own: its hot path is a set of MATLAB functions resolved by name
+ * (rho1.m, rho2.m, rho3.m, A.m, B.m, Rho_to_PhiGammaLambda.m, getWLc.m and
+ * MathWorks quadprog).  Function-handle arguments cannot cross a C ABI, so the
+ * boundary sits at the time-step level (one MEX call replaces lines 94-130 for
+ * a whole batch of scenarios) plus one entry point per reference function for
+ * per-function parity.  See INTEGRATION.md for the MEX / ctypes bindings.
+ *
+ * Conventions
+ *  - fp64 everywhere; all per-scenario matrices are MATLAB column-major.
+ *  - Batched arrays are scenario-minor ("SoA"): element e of scenario s lives
+ *    at [e*B + s].  In MATLAB this is simply a B-by-E array.
+ *  - Host-pointer entry points (no suffix) stage through the device and are
+ *    synchronous.  *_device entry points take device pointers and a
+ *    hipStream_t (as void*), enqueue only, and never synchronise.
+ *  - Return value: NTM_OK (0) or a negative NTM_E_* code; the message is in
+ *    ntm_last_error(ctx).  Per-scenario solver outcomes are NOT errors: they
+ *    are reported in exitflag[] with quadprog's codes (NTM_MPC_Sim.m:98-103).
+ *  - Caller owns every array; the library never retains a pointer past the
+ *    call.  One call at a time per ntm_ctx.
+ */
+#ifndef NTM_MPC_H
+#define NTM_MPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NTM_MPC_ABI_VERSION 1
+#define NTM_MAX_N 64
+
+/* Physics constants, NTM_MPC_Sim.m:5-22 (same names and units). */
+typedef struct {
+    double j_BS, w_dep, w_marg, w_sat, tau_r, rs, a, eta_CD, tau_E0, tau_E,
+           mu0, Lq, B_pol, m, Cw, tau_A0, tau_w, omega0;
+} ntm_physics;
+
+/* Constraint modes. */
+enum { NTM_MODE_NONE = 0,   /* unconstrained LQ (BASELINE config 1)       */
+       NTM_MODE_BOX = 1,    /* u in [umin, umax] only (config 2)          */
+       NTM_MODE_FULL = 2 }; /* full getWLc.m polyhedron, m = 6N+4 (cfg 3) */
+
+/* Literal-reference switches; 0 = canonical semantics. */
+enum { NTM_LITERAL_PHI_RIGHTMUL = 1 << 0,  /* D4  Rho_to_PhiGammaLambda.m:21 */
+       NTM_LITERAL_GAMMA_INDEX = 1 << 1,   /* D6  Rho_to_PhiGammaLambda.m:32 */
+       NTM_LITERAL_PLANT_NO_C = 1 << 2,    /* D13 NTM_MPC_Sim.m:130          */
+       NTM_RHO1_SQUARED = 1 << 3 };        /* D18 rhos.m:18                  */
+
+/* Controller configuration, NTM_MPC_Sim.m:30-60, 80-88. */
+typedef struct {
+    int32_t N;          /* :30 prediction horizon, 1..NTM_MAX_N            */
+    int32_t i_sim;      /* :81 max LPV scheduling iterations               */
+    int32_t mode;       /* NTM_MODE_*                                      */
+    int32_t flags;      /* NTM_LITERAL_* / NTM_RHO1_SQUARED                */
+    double Ts;          /* :31                                             */
+    double xmin[2];     /* :44                                             */
+    double xmax[2];     /* :45                                             */
+    double umin, umax;  /* :49-50                                          */
+    double Q[4];        /* :59 state weight, row-major 2x2, symmetric PSD  */
+    double r[2];        /* :60 reference state                             */
+    double epsilon;     /* :87 convergence threshold on sum|U - Uold|      */
+} ntm_config;
+
+/* Return codes. */
+enum { NTM_OK = 0, NTM_E_INVALID = -1, NTM_E_DEVICE = -2, NTM_E_NOMEM = -3,
+       NTM_E_UNSUPPORTED = -4 };
+
+/* Per-scenario QP exit flags (quadprog convention, NTM_MPC_Sim.m:98-103). */
+enum { NTM_EXIT_OPTIMAL = 1, NTM_EXIT_MAXITER = 0, NTM_EXIT_INFEASIBLE = -2,
+       NTM_EXIT_NONFINITE = -7 };
+
+/* Defaults = the reference's hard-coded literals (NTM_MPC_Sim.m:5-88). */
+void ntm_physics_default(ntm_physics* p);
+void ntm_config_default(ntm_config* c, int32_t N);
+int32_t ntm_abi_version(void);
+
+typedef struct ntm_ctx ntm_ctx;
+int ntm_ctx_create(ntm_ctx** out, int32_t device);
+void ntm_ctx_destroy(ntm_ctx* ctx);
+const char* ntm_last_error(const ntm_ctx* ctx);
+
+/* ---- time-step level: the drop-in for NTM_MPC_Sim.m:94-130 ------------ */
+/* One MPC step for B scenarios.  In/out state per scenario:
+ *   x_k[2], rho[3N] (3xN col-major: rows rho1,rho2,rho3; carried unshifted,
+ *   D20), U_old[N] (persists across steps, D14; +inf on the first step).
+ * Outputs: U[N] (last QP solve), x_pred[2(N+1)] (2x(N+1) rollout x_0..x_N),
+ *   x_next[2] (plant step :130), exitflag (last QP), inner_iters (QP solves). */
+int ntm_mpc_step(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg,
+                 int64_t B, const double* x_k, double* rho, double* U_old,
+                 double* U, double* x_pred, double* x_next,
+                 int32_t* exitflag, int32_t* inner_iters);
+int ntm_mpc_step_device(ntm_ctx* ctx, const ntm_physics* phys,
+                        const ntm_config* cfg, int64_t B, const double* x_k,
+                        double* rho, double* U_old, double* U, double* x_pred,
+                        double* x_next, int32_t* exitflag, int32_t* inner_iters,
+                        void* stream);
+
+/* Closed loop NTM_MPC_Sim.m:80-131 over k_sim steps, device-resident.
+ * x0[2]; outputs xk[2(k_sim+1)] (2x(k_sim+1)), uk[k_sim], Uk[N k_sim]
+ * (N x k_sim), wpred[(N+1) k_sim] (predicted island width per step),
+ * exitflag[k_sim], inner_iters[k_sim].  Any output pointer may be NULL. */
+int ntm_mpc_run(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg,
+                int64_t B, int32_t k_sim, const double* x0, double* xk,
+                double* uk, double* Uk, double* wpred, int32_t* exitflag,
+                int32_t* inner_iters);
+int ntm_mpc_run_device(ntm_ctx* ctx, const ntm_physics* phys,
+                       const ntm_config* cfg, int64_t B, int32_t k_sim,
+                       const double* x0, double* xk, double* uk, double* Uk,
+                       double* wpred, int32_t* exitflag, int32_t* inner_iters,
+                       void* stream);
+
+/* ---- function level: one entry per reference function (device ptrs) --- */
+/* rho1.m / rho2.m / rho3.m at x[2] -> rho[3]. */
+int ntm_rho_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg,
+                   int64_t B, const double* x, double* rho, void* stream);
+/* A.m / B.m at rho[3] -> A[4] (2x2 col-major), Bv[2] (2x1 column, D5). */
+int ntm_AB_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg,
+                  int64_t B, const double* rho, double* A, double* Bv,
+                  void* stream);
+/* Rho_to_PhiGammaLambda.m: rho[3N] -> Phi[2N*2], Gamma[2N*N], Lambda[2N]. */
+int ntm_lift_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg,
+                    int64_t B, const double* rho, double* Phi, double* Gamma,
+                    double* Lambda, void* stream);
+/* NTM_MPC_Sim.m:120-121: (rho, x_k) -> G[N*N], F[N]. */
+int ntm_cost_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg,
+                    int64_t B, const double* rho, const double* x_k, double* G,
+                    double* F, void* stream);
+/* getWLc.m: rho -> W[m*2], L[m*N], c[m], m = 6N+4. */
+int ntm_getwlc_device(ntm_ctx* ctx, const ntm_physics* phys,
+                      const ntm_config* cfg, int64_t B, const double* rho,
+                      double* W, double* L, double* c, void* stream);
+/* quadprog stand-in (NTM_MPC_Sim.m:97): min 1/2 U'GU + F'U s.t. Lin U <= b,
+ * G[N*N], F[N], Lin[m*N], b[m] per scenario -> U[N], exitflag. */
+int ntm_qp_device(ntm_ctx* ctx, int64_t B, int32_t N, int32_t m,
+                  const double* G, const double* F, const double* Lin,
+                  const double* b, double* U, int32_t* exitflag,
+                  int32_t* iters, void* stream);
+
+/* Synthetic scenarios, counter-based and shard-invariant:
+ * x0 for global scenario ids first_id .. first_id+B-1 (host array 2xB SoA). */
+void ntm_scenarios_x0(uint64_t seed, int64_t first_id, int64_t B, double* x0);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NTM_MPC_H */

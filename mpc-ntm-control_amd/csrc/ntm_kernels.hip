@@ -1,0 +1,707 @@
+// ntm_kernels.hip — HIP kernels (gfx950) and the C-ABI of include/ntm_mpc.h.
+//
+// Hot path: k_mpc_step / k_mpc_run — one fused launch per MPC time step (or
+// per closed loop) for the whole scenario batch.  Each group of P lanes runs
+// the complete NTM_MPC_Sim.m:94-130 body for one scenario out of LDS:
+// lift -> cost -> Jacobi scaling -> Goldfarb-Idnani QP -> rollout / rho update
+// -> convergence test, i_sim times, then the plant step.  Nothing but the
+// per-scenario state (x_k, rho, U_old) and the outputs touches HBM.
+//
+// The remaining kernels are the function-level entry points (one per MATLAB
+// function) used by the per-function parity tests; they reuse the very same
+// device phases.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "ntm_device.h"
+
+using namespace ntm;
+
+namespace {
+
+template <int P>
+__device__ __forceinline__ void load_state(const WS& w, int64_t B, int64_t s, const double* rho,
+                                           const double* U_old, int l) {
+    const int N = w.N;
+    for (int e = l; e < 3 * N; e += P) w.rho[e] = rho[(int64_t)e * B + s];
+    if (l < N) w.Uold[l] = U_old[(int64_t)l * B + s];
+    NTM_WSYNC();
+}
+
+// one MPC step on LDS-resident state; returns exit flag, sets *iters
+template <int P>
+__device__ int mpc_step_dev(const Prob& pb, const WS& w, double x0, double x1, int l, int* iters) {
+    int flag = NTM_EXIT_OPTIMAL, it;
+    for (it = 1; it <= pb.i_sim; ++it) {
+        int qi;
+        flag = qp_phase<P>(pb, w, x0, x1, l, &qi);
+        if (rollout_phase<P>(pb, w, x0, x1, l)) break;
+    }
+    *iters = it > pb.i_sim ? pb.i_sim : it;
+    return flag;
+}
+
+template <int P>
+__global__ __launch_bounds__(64) void k_mpc_step(Prob pb, int64_t B, const double* __restrict__ x_k,
+                                                 double* __restrict__ rho, double* __restrict__ U_old,
+                                                 double* __restrict__ U, double* __restrict__ x_pred,
+                                                 double* __restrict__ x_next, int32_t* __restrict__ exitflag,
+                                                 int32_t* __restrict__ inner_iters) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int G = 64 / P;
+    const int g = threadIdx.x / P, l = threadIdx.x % P;
+    const int64_t s = (int64_t)blockIdx.x * G + g;
+    const int N = pb.N;
+    if (s >= B) return;
+    WS w = ws_carve(smem + g * ws_bytes(N), N);
+    const double x0 = x_k[s], x1 = x_k[B + s];
+    load_state<P>(w, B, s, rho, U_old, l);
+    int its;
+    int flag = mpc_step_dev<P>(pb, w, x0, x1, l, &its);
+    for (int e = l; e < 3 * N; e += P) rho[(int64_t)e * B + s] = w.rho[e];
+    if (l < N) {
+        U_old[(int64_t)l * B + s] = w.Uold[l];
+        U[(int64_t)l * B + s] = w.U[l];
+    }
+    for (int e = l; e < 2 * (N + 1); e += P) x_pred[(int64_t)e * B + s] = w.xp[e];
+    if (l == 0) {
+        double n0, n1;
+        plant_step(pb, x0, x1, w.U[0], n0, n1);
+        x_next[s] = n0;
+        x_next[B + s] = n1;
+        exitflag[s] = flag;
+        inner_iters[s] = its;
+    }
+}
+
+template <int P>
+__global__ __launch_bounds__(64) void k_mpc_run(Prob pb, int64_t B, int k_sim, const double* __restrict__ x0v,
+                                                double* xk, double* uk, double* Uk, double* wpred,
+                                                int32_t* exitflag, int32_t* inner_iters) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int G = 64 / P;
+    const int g = threadIdx.x / P, l = threadIdx.x % P;
+    const int64_t s = (int64_t)blockIdx.x * G + g;
+    const int N = pb.N;
+    if (s >= B) return;
+    WS w = ws_carve(smem + g * ws_bytes(N), N);
+    double x0 = x0v[s], x1 = x0v[B + s];
+    {   // Rho = repmat(rho(x0), 1, N) (NTM_MPC_Sim.m:63-65); Uold = +inf (D14)
+        double r1, r2, r3;
+        rho_eval(pb.k, x0, x1, r1, r2, r3);
+        if (l < N) {
+            w.rho[3 * l] = r1;
+            w.rho[3 * l + 1] = r2;
+            w.rho[3 * l + 2] = r3;
+            w.Uold[l] = kInf;
+        }
+        NTM_WSYNC();
+    }
+    if (xk && l == 0) { xk[s] = x0; xk[B + s] = x1; }
+    for (int kk = 0; kk < k_sim; ++kk) {
+        int its;
+        int flag = mpc_step_dev<P>(pb, w, x0, x1, l, &its);
+        if (Uk && l < N) Uk[((int64_t)kk * N + l) * B + s] = w.U[l];
+        if (wpred) for (int i = l; i <= N; i += P) wpred[((int64_t)kk * (N + 1) + i) * B + s] = w.xp[2 * i];
+        double n0, n1;
+        plant_step(pb, x0, x1, w.U[0], n0, n1);
+        if (l == 0) {
+            if (uk) uk[(int64_t)kk * B + s] = w.U[0];
+            if (exitflag) exitflag[(int64_t)kk * B + s] = flag;
+            if (inner_iters) inner_iters[(int64_t)kk * B + s] = its;
+            if (xk) { xk[(int64_t)(2 * kk + 2) * B + s] = n0; xk[(int64_t)(2 * kk + 3) * B + s] = n1; }
+        }
+        x0 = n0;
+        x1 = n1;
+        NTM_WSYNC();
+    }
+}
+
+// ---------------------------------------------------------------- building blocks
+__global__ void k_rho(Prob pb, int64_t B, const double* x, double* rho) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    double r1, r2, r3;
+    rho_eval(pb.k, x[s], x[B + s], r1, r2, r3);
+    rho[s] = r1;
+    rho[B + s] = r2;
+    rho[2 * B + s] = r3;
+}
+
+__global__ void k_AB(Prob pb, int64_t B, const double* rho, double* A, double* Bv) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    double a11 = coef_a11(pb.k, rho[s]), a21 = coef_a21(pb.k, rho[B + s]), b = coef_b(pb.k, rho[2 * B + s]);
+    A[s] = a11;
+    A[B + s] = a21;
+    A[2 * B + s] = 0.0;
+    A[3 * B + s] = pb.k.a22;
+    Bv[s] = b;
+    Bv[B + s] = 0.0;
+}
+
+template <int P>
+__global__ __launch_bounds__(64) void k_lift(Prob pb, int64_t B, const double* rho, double* Phi, double* Gam,
+                                             double* Lam) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int G = 64 / P;
+    const int g = threadIdx.x / P, l = threadIdx.x % P;
+    const int64_t s = (int64_t)blockIdx.x * G + g;
+    const int N = pb.N, R = 2 * N;
+    if (s >= B) return;
+    WS w = ws_carve(smem + g * ws_bytes(N), N);
+    for (int e = l; e < 3 * N; e += P) w.rho[e] = rho[(int64_t)e * B + s];
+    NTM_WSYNC();
+    lift_phase<P>(pb, w, l);
+    for (int i = l; i < N; i += P) {
+        const double* Ph = w.Phi + 4 * i;
+        Phi[(int64_t)(2 * i) * B + s] = Ph[0];
+        Phi[(int64_t)(2 * i + 1) * B + s] = Ph[1];
+        Phi[(int64_t)(R + 2 * i) * B + s] = Ph[2];
+        Phi[(int64_t)(R + 2 * i + 1) * B + s] = Ph[3];
+        Lam[(int64_t)(2 * i) * B + s] = w.Lam[2 * i];
+        Lam[(int64_t)(2 * i + 1) * B + s] = w.Lam[2 * i + 1];
+    }
+    for (int e = l; e < R * N; e += P) Gam[(int64_t)e * B + s] = w.Gt[e];
+}
+
+template <int P>
+__global__ __launch_bounds__(64) void k_cost(Prob pb, int64_t B, const double* rho, const double* x,
+                                             double* G_out, double* F_out) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int G = 64 / P;
+    const int g = threadIdx.x / P, l = threadIdx.x % P;
+    const int64_t s = (int64_t)blockIdx.x * G + g;
+    const int N = pb.N;
+    if (s >= B) return;
+    WS w = ws_carve(smem + g * ws_bytes(N), N);
+    for (int e = l; e < 3 * N; e += P) w.rho[e] = rho[(int64_t)e * B + s];
+    NTM_WSYNC();
+    lift_phase<P>(pb, w, l);
+    free_response<P>(w, x[s], x[B + s], l);
+    cost_phase<P>(pb, w, l);
+    if (l < N) {
+        for (int kk = 0; kk <= l; ++kk) {
+            double v = w.R[l + kk * w.LDJ];
+            G_out[(int64_t)(l + kk * N) * B + s] = v;
+            G_out[(int64_t)(kk + l * N) * B + s] = v;
+        }
+        F_out[(int64_t)l * B + s] = w.F[l];
+    }
+}
+
+// getWLc.m:9-59 materialised (for parity only; the hot path never builds it)
+template <int P>
+__global__ __launch_bounds__(64) void k_getwlc(Prob pb, int64_t B, const double* rho, double* W, double* L,
+                                               double* c) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int G = 64 / P;
+    const int g = threadIdx.x / P, l = threadIdx.x % P;
+    const int64_t s = (int64_t)blockIdx.x * G + g;
+    const int N = pb.N, m = 6 * N + 4;
+    if (s >= B) return;
+    WS w = ws_carve(smem + g * ws_bytes(N), N);
+    for (int e = l; e < 3 * N; e += P) w.rho[e] = rho[(int64_t)e * B + s];
+    NTM_WSYNC();
+    lift_phase<P>(pb, w, l);
+    for (int row = l; row < m; row += P) {
+        int blk = row / 6, rr = row - 6 * blk;
+        double Wr0 = 0.0, Wr1 = 0.0, cr = 0.0;
+        for (int j = 0; j < N; ++j) L[((int64_t)row + (int64_t)j * m) * B + s] = 0.0;
+        bool urow = blk < N && rr < 2;
+        if (urow) {
+            L[((int64_t)row + (int64_t)blk * m) * B + s] = (rr == 0) ? -1.0 : 1.0;
+            cr = (rr == 0) ? -pb.umin : pb.umax;
+        } else {
+            int i, cc;
+            bool upper;
+            if (blk < N) { i = blk; cc = (rr - 2) & 1; upper = rr >= 4; }
+            else { i = N; cc = rr & 1; upper = rr >= 2; }
+            double sg = upper ? 1.0 : -1.0;
+            cr = upper ? pb.xmax[cc] : -pb.xmin[cc];
+            if (i == 0) {                     // Dcal rows: W = -Mi
+                if (cc == 0) Wr0 = -sg; else Wr1 = -sg;
+            } else {
+                int r = 2 * (i - 1) + cc;
+                for (int j = 0; j < N; ++j) L[((int64_t)row + (int64_t)j * m) * B + s] = sg * w.Gt[r + j * w.LDG];
+                Wr0 = -sg * w.Phi[4 * (i - 1) + cc];
+                Wr1 = -sg * w.Phi[4 * (i - 1) + 2 + cc];
+                cr -= sg * w.Lam[r];
+            }
+        }
+        W[(int64_t)row * B + s] = Wr0;
+        W[(int64_t)(m + row) * B + s] = Wr1;
+        c[(int64_t)row * B + s] = cr;
+    }
+}
+
+// quadprog stand-in on explicit data (dense rows)
+template <int P>
+__global__ __launch_bounds__(64) void k_qp(int64_t B, int N, int m, const double* G_in, const double* F_in,
+                                           const double* Lin, const double* b, double* U, int32_t* exitflag,
+                                           int32_t* iters) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int G = 64 / P;
+    const int g = threadIdx.x / P, l = threadIdx.x % P;
+    const int64_t s = (int64_t)blockIdx.x * G + g;
+    if (s >= B) return;
+    const int wsb = ws_bytes(N) + ((m * 8 + 15) & ~15);
+    char* base = smem + g * wsb;
+    WS w = ws_carve(base, N);
+    double* rnrm = reinterpret_cast<double*>(base + ws_bytes(N));
+    if (l < N) {
+        for (int kk = 0; kk <= l; ++kk) w.R[l + kk * w.LDJ] = G_in[((int64_t)l + (int64_t)kk * N) * B + s];
+        w.F[l] = F_in[(int64_t)l * B + s];
+    }
+    for (int i = l; i < m; i += P) w.aflag[i] = 0;
+    NTM_WSYNC();
+    int flag, its = 0;
+    if (!scale_phase<P>(w, l, false)) {
+        flag = NTM_EXIT_NONFINITE;
+    } else {
+        DenseRows rows{Lin, b, rnrm, B, s, m};
+        int code = rows.template prepare_code<P>(w, l);
+        if (code & 1) flag = NTM_EXIT_NONFINITE;
+        else if (code & 2) flag = NTM_EXIT_INFEASIBLE;
+        else flag = gi_solve<P, DenseRows>(w, m > 0 ? &rows : nullptr, m, l, &its);
+    }
+    if (l < N) {
+        double u = (flag == NTM_EXIT_OPTIMAL || flag == NTM_EXIT_MAXITER) ? w.V[l] * w.D[l] : 0.0;
+        U[(int64_t)l * B + s] = u;
+    }
+    if (l == 0) {
+        exitflag[s] = flag;
+        if (iters) iters[s] = its;
+    }
+}
+
+// ------------------------------------------------------------------ host helpers
+Prob make_prob(const ntm_physics* p, const ntm_config* c) {
+    // identical expressions to oracle/ntm_oracle.c orc_coeffs (NTM_MPC_Sim.m:24-25, 37; A.m; B.m)
+    const double pi = 3.14159265358979323846;
+    double kappa = 16 * p->mu0 * p->Lq * (p->rs * p->rs) / (0.82 * p->tau_r * p->B_pol * pi);
+    double zeta = p->m * p->Cw * (p->tau_A0 * p->tau_A0) * p->tau_w * (p->a * p->a * p->a);
+    Prob pb;
+    std::memset(&pb, 0, sizeof(pb));
+    double Ts = c->Ts;
+    pb.k.a11c = (4.0 / 3.0) * (kappa * p->rs / (0.82 * p->tau_r)) * Ts;
+    pb.k.za3 = zeta * (p->a * p->a * p->a);
+    pb.k.a22 = 1 - Ts / p->tau_E;
+    pb.k.bc = (kappa * Ts * p->eta_CD / p->w_dep);
+    pb.k.C1 = -4.0 / 3.0 * (kappa * Ts * p->j_BS * p->w_sat) / (p->w_sat * p->w_sat + p->w_marg * p->w_marg);
+    pb.k.C2 = Ts * p->omega0 / p->tau_E0;
+    pb.k.wmarg2 = p->w_marg * p->w_marg;
+    pb.k.wdep = p->w_dep;
+    pb.k.Ts = Ts;
+    pb.k.rho1_sq = (c->flags & NTM_RHO1_SQUARED) != 0;
+    pb.N = c->N;
+    pb.i_sim = c->i_sim;
+    pb.mode = c->mode;
+    pb.flags = c->flags;
+    for (int i = 0; i < 2; ++i) {
+        pb.xmin[i] = c->xmin[i];
+        pb.xmax[i] = c->xmax[i];
+        pb.r[i] = c->r[i];
+    }
+    pb.umin = c->umin;
+    pb.umax = c->umax;
+    for (int i = 0; i < 4; ++i) pb.Q[i] = c->Q[i];
+    pb.eps = c->epsilon;
+    return pb;
+}
+
+int lanes_for(int N) { return N <= 16 ? 16 : (N <= 32 ? 32 : 64); }
+
+}  // namespace
+
+// =========================================================================
+// C-ABI
+// =========================================================================
+struct ntm_ctx {
+    int device = 0;
+    std::string err;
+    void* dbuf = nullptr;
+    size_t dbuf_bytes = 0;
+    hipStream_t stream = nullptr;
+};
+
+namespace {
+
+int fail(ntm_ctx* ctx, int code, const std::string& msg) {
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+int check_hip(ntm_ctx* ctx, hipError_t e, const char* what) {
+    if (e == hipSuccess) return NTM_OK;
+    return fail(ctx, NTM_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int validate(ntm_ctx* ctx, const ntm_physics* p, const ntm_config* c, int64_t B) {
+    if (!ctx) return NTM_E_INVALID;
+    if (!p || !c) return fail(ctx, NTM_E_INVALID, "null physics/config");
+    if (c->N < 1 || c->N > NTM_MAX_N) return fail(ctx, NTM_E_INVALID, "N out of range [1, 64]");
+    if (c->i_sim < 1) return fail(ctx, NTM_E_INVALID, "i_sim must be >= 1");
+    if (c->mode < NTM_MODE_NONE || c->mode > NTM_MODE_FULL) return fail(ctx, NTM_E_INVALID, "bad mode");
+    if (B < 0) return fail(ctx, NTM_E_INVALID, "negative batch");
+    return NTM_OK;
+}
+
+template <typename K>
+int set_lds(ntm_ctx* ctx, K kern, size_t lds) {
+    if (lds > 160 * 1024) return fail(ctx, NTM_E_UNSUPPORTED, "LDS workspace exceeds 160 KiB");
+    if (lds > 64 * 1024)
+        return check_hip(ctx,
+                         hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds),
+                         "hipFuncSetAttribute");
+    return NTM_OK;
+}
+
+template <int P>
+int launch_step(ntm_ctx* ctx, const Prob& pb, int64_t B, const double* x_k, double* rho, double* U_old,
+                double* U, double* x_pred, double* x_next, int32_t* exitflag, int32_t* inner_iters,
+                hipStream_t st) {
+    constexpr int G = 64 / P;
+    size_t lds = (size_t)G * ws_bytes(pb.N);
+    int rc = set_lds(ctx, k_mpc_step<P>, lds);
+    if (rc) return rc;
+    int64_t blocks = (B + G - 1) / G;
+    if (blocks == 0) return NTM_OK;
+    hipLaunchKernelGGL(k_mpc_step<P>, dim3((unsigned)blocks), dim3(64), lds, st, pb, B, x_k, rho, U_old, U,
+                       x_pred, x_next, exitflag, inner_iters);
+    return check_hip(ctx, hipGetLastError(), "k_mpc_step launch");
+}
+
+template <int P>
+int launch_run(ntm_ctx* ctx, const Prob& pb, int64_t B, int k_sim, const double* x0, double* xk, double* uk,
+               double* Uk, double* wpred, int32_t* exitflag, int32_t* inner_iters, hipStream_t st) {
+    constexpr int G = 64 / P;
+    size_t lds = (size_t)G * ws_bytes(pb.N);
+    int rc = set_lds(ctx, k_mpc_run<P>, lds);
+    if (rc) return rc;
+    int64_t blocks = (B + G - 1) / G;
+    if (blocks == 0) return NTM_OK;
+    hipLaunchKernelGGL(k_mpc_run<P>, dim3((unsigned)blocks), dim3(64), lds, st, pb, B, k_sim, x0, xk, uk, Uk,
+                       wpred, exitflag, inner_iters);
+    return check_hip(ctx, hipGetLastError(), "k_mpc_run launch");
+}
+
+#define NTM_DISPATCH_P(N, CALL) \
+    (lanes_for(N) == 16 ? CALL(16) : (lanes_for(N) == 32 ? CALL(32) : CALL(64)))
+
+struct DevBuf {
+    ntm_ctx* ctx;
+    char* cur;
+    char* end;
+};
+
+int ensure_buf(ntm_ctx* ctx, size_t bytes) {
+    if (ctx->dbuf_bytes >= bytes) return NTM_OK;
+    if (ctx->dbuf) (void)hipFree(ctx->dbuf);
+    ctx->dbuf = nullptr;
+    ctx->dbuf_bytes = 0;
+    int rc = check_hip(ctx, hipMalloc(&ctx->dbuf, bytes), "hipMalloc");
+    if (rc) return fail(ctx, NTM_E_NOMEM, ctx->err);
+    ctx->dbuf_bytes = bytes;
+    return NTM_OK;
+}
+
+size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
+
+}  // namespace
+
+extern "C" {
+
+void ntm_physics_default(ntm_physics* p) {
+    // NTM_MPC_Sim.m:5-22
+    p->j_BS = 73e3;
+    p->w_dep = 0.024;
+    p->w_marg = 0.02;
+    p->w_sat = 0.32;
+    p->tau_r = 293;
+    p->rs = 1.55;
+    p->a = 2.0;
+    p->eta_CD = 0.9;
+    p->tau_E0 = 3.7;
+    p->tau_E = p->tau_E0;
+    p->mu0 = 4e-7 * 3.14159265358979323846;
+    p->Lq = 0.87;
+    p->B_pol = 0.97;
+    p->m = 2;
+    p->Cw = 1;
+    p->tau_A0 = 3e-6;
+    p->tau_w = 0.188;
+    p->omega0 = 2 * 3.14159265358979323846 * 420;
+}
+
+void ntm_config_default(ntm_config* c, int32_t N) {
+    // NTM_MPC_Sim.m:30-60, 80-88
+    const double pi = 3.14159265358979323846;
+    std::memset(c, 0, sizeof(*c));
+    c->N = N;
+    c->i_sim = 10;
+    c->mode = NTM_MODE_FULL;
+    c->flags = 0;
+    c->Ts = 0.1;
+    c->xmin[0] = 0.06;
+    c->xmin[1] = 100 * 2 * pi;
+    c->xmax[0] = 0.15;
+    c->xmax[1] = 5000 * 2 * pi;
+    c->umin = 0;
+    c->umax = 2e6;
+    c->Q[0] = 1; c->Q[1] = 0; c->Q[2] = 0; c->Q[3] = 1;
+    c->r[0] = 0;
+    c->r[1] = 1000 * 2 * pi;
+    c->epsilon = 1e-14;
+}
+
+int32_t ntm_abi_version(void) { return NTM_MPC_ABI_VERSION; }
+
+int ntm_ctx_create(ntm_ctx** out, int32_t device) {
+    if (!out) return NTM_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return NTM_E_DEVICE;
+    if (device < 0 || device >= n) return NTM_E_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return NTM_E_DEVICE;
+    ntm_ctx* c = new ntm_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return NTM_E_DEVICE;
+    }
+    *out = c;
+    return NTM_OK;
+}
+
+void ntm_ctx_destroy(ntm_ctx* ctx) {
+    if (!ctx) return;
+    if (ctx->dbuf) (void)hipFree(ctx->dbuf);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* ntm_last_error(const ntm_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int ntm_mpc_step_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B,
+                        const double* x_k, double* rho, double* U_old, double* U, double* x_pred, double* x_next,
+                        int32_t* exitflag, int32_t* inner_iters, void* stream) {
+    int rc = validate(ctx, phys, cfg, B);
+    if (rc) return rc;
+    if (B == 0) return NTM_OK;
+    if (!x_k || !rho || !U_old || !U || !x_pred || !x_next || !exitflag || !inner_iters)
+        return fail(ctx, NTM_E_INVALID, "null array");
+    Prob pb = make_prob(phys, cfg);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define CALL(P) launch_step<P>(ctx, pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, st)
+    return NTM_DISPATCH_P(cfg->N, CALL);
+#undef CALL
+}
+
+int ntm_mpc_step(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* x_k,
+                 double* rho, double* U_old, double* U, double* x_pred, double* x_next, int32_t* exitflag,
+                 int32_t* inner_iters) {
+    int rc = validate(ctx, phys, cfg, B);
+    if (rc) return rc;
+    if (B == 0) return NTM_OK;
+    if (!x_k || !rho || !U_old || !U || !x_pred || !x_next || !exitflag || !inner_iters)
+        return fail(ctx, NTM_E_INVALID, "null array");
+    const int N = cfg->N;
+    size_t bx = al(2 * B * 8), brho = al(3 * N * B * 8), bu = al(N * B * 8), bxp = al(2 * (N + 1) * B * 8),
+           bi = al(B * 4);
+    rc = ensure_buf(ctx, bx * 2 + brho + bu * 2 + bxp + bi * 2);
+    if (rc) return rc;
+    char* p = static_cast<char*>(ctx->dbuf);
+    double* dx = (double*)p; p += bx;
+    double* drho = (double*)p; p += brho;
+    double* duo = (double*)p; p += bu;
+    double* dU = (double*)p; p += bu;
+    double* dxp = (double*)p; p += bxp;
+    double* dxn = (double*)p; p += bx;
+    int32_t* dfl = (int32_t*)p; p += bi;
+    int32_t* dit = (int32_t*)p;
+    hipStream_t st = ctx->stream;
+    if ((rc = check_hip(ctx, hipMemcpyAsync(dx, x_k, 2 * B * 8, hipMemcpyHostToDevice, st), "H2D"))) return rc;
+    if ((rc = check_hip(ctx, hipMemcpyAsync(drho, rho, 3 * N * B * 8, hipMemcpyHostToDevice, st), "H2D"))) return rc;
+    if ((rc = check_hip(ctx, hipMemcpyAsync(duo, U_old, N * B * 8, hipMemcpyHostToDevice, st), "H2D"))) return rc;
+    rc = ntm_mpc_step_device(ctx, phys, cfg, B, dx, drho, duo, dU, dxp, dxn, dfl, dit, st);
+    if (rc) return rc;
+    if ((rc = check_hip(ctx, hipMemcpyAsync(rho, drho, 3 * N * B * 8, hipMemcpyDeviceToHost, st), "D2H"))) return rc;
+    if ((rc = check_hip(ctx, hipMemcpyAsync(U_old, duo, N * B * 8, hipMemcpyDeviceToHost, st), "D2H"))) return rc;
+    if ((rc = check_hip(ctx, hipMemcpyAsync(U, dU, N * B * 8, hipMemcpyDeviceToHost, st), "D2H"))) return rc;
+    if ((rc = check_hip(ctx, hipMemcpyAsync(x_pred, dxp, 2 * (N + 1) * B * 8, hipMemcpyDeviceToHost, st), "D2H")))
+        return rc;
+    if ((rc = check_hip(ctx, hipMemcpyAsync(x_next, dxn, 2 * B * 8, hipMemcpyDeviceToHost, st), "D2H"))) return rc;
+    if ((rc = check_hip(ctx, hipMemcpyAsync(exitflag, dfl, B * 4, hipMemcpyDeviceToHost, st), "D2H"))) return rc;
+    if ((rc = check_hip(ctx, hipMemcpyAsync(inner_iters, dit, B * 4, hipMemcpyDeviceToHost, st), "D2H"))) return rc;
+    return check_hip(ctx, hipStreamSynchronize(st), "sync");
+}
+
+int ntm_mpc_run_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, int32_t k_sim,
+                       const double* x0, double* xk, double* uk, double* Uk, double* wpred, int32_t* exitflag,
+                       int32_t* inner_iters, void* stream) {
+    int rc = validate(ctx, phys, cfg, B);
+    if (rc) return rc;
+    if (k_sim < 0) return fail(ctx, NTM_E_INVALID, "negative k_sim");
+    if (B == 0) return NTM_OK;
+    if (!x0) return fail(ctx, NTM_E_INVALID, "null x0");
+    Prob pb = make_prob(phys, cfg);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define CALL(P) launch_run<P>(ctx, pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, st)
+    return NTM_DISPATCH_P(cfg->N, CALL);
+#undef CALL
+}
+
+int ntm_mpc_run(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, int32_t k_sim,
+                const double* x0, double* xk, double* uk, double* Uk, double* wpred, int32_t* exitflag,
+                int32_t* inner_iters) {
+    int rc = validate(ctx, phys, cfg, B);
+    if (rc) return rc;
+    if (k_sim < 0) return fail(ctx, NTM_E_INVALID, "negative k_sim");
+    if (B == 0) return NTM_OK;
+    const int N = cfg->N;
+    size_t b0 = al(2 * B * 8), bxk = al(2 * (size_t)(k_sim + 1) * B * 8), buk = al((size_t)k_sim * B * 8),
+           bUk = al((size_t)N * k_sim * B * 8), bwp = al((size_t)(N + 1) * k_sim * B * 8),
+           bi = al((size_t)k_sim * B * 4);
+    rc = ensure_buf(ctx, b0 + bxk + buk + bUk + bwp + 2 * bi);
+    if (rc) return rc;
+    char* p = static_cast<char*>(ctx->dbuf);
+    double* d0 = (double*)p; p += b0;
+    double* dxk = (double*)p; p += bxk;
+    double* duk = (double*)p; p += buk;
+    double* dUk = (double*)p; p += bUk;
+    double* dwp = (double*)p; p += bwp;
+    int32_t* dfl = (int32_t*)p; p += bi;
+    int32_t* dit = (int32_t*)p;
+    hipStream_t st = ctx->stream;
+    if ((rc = check_hip(ctx, hipMemcpyAsync(d0, x0, 2 * B * 8, hipMemcpyHostToDevice, st), "H2D"))) return rc;
+    rc = ntm_mpc_run_device(ctx, phys, cfg, B, k_sim, d0, xk ? dxk : nullptr, uk ? duk : nullptr,
+                            Uk ? dUk : nullptr, wpred ? dwp : nullptr, exitflag ? dfl : nullptr,
+                            inner_iters ? dit : nullptr, st);
+    if (rc) return rc;
+    struct { void* h; void* d; size_t n; } outs[] = {
+        {xk, dxk, 2 * (size_t)(k_sim + 1) * B * 8}, {uk, duk, (size_t)k_sim * B * 8},
+        {Uk, dUk, (size_t)N * k_sim * B * 8},        {wpred, dwp, (size_t)(N + 1) * k_sim * B * 8},
+        {exitflag, dfl, (size_t)k_sim * B * 4},      {inner_iters, dit, (size_t)k_sim * B * 4}};
+    for (auto& o : outs)
+        if (o.h && (rc = check_hip(ctx, hipMemcpyAsync(o.h, o.d, o.n, hipMemcpyDeviceToHost, st), "D2H")))
+            return rc;
+    return check_hip(ctx, hipStreamSynchronize(st), "sync");
+}
+
+int ntm_rho_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* x,
+                   double* rho, void* stream) {
+    int rc = validate(ctx, phys, cfg, B);
+    if (rc || B == 0) return rc;
+    Prob pb = make_prob(phys, cfg);
+    hipLaunchKernelGGL(k_rho, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, (hipStream_t)stream, pb, B, x, rho);
+    return check_hip(ctx, hipGetLastError(), "k_rho");
+}
+
+int ntm_AB_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* rho,
+                  double* A, double* Bv, void* stream) {
+    int rc = validate(ctx, phys, cfg, B);
+    if (rc || B == 0) return rc;
+    Prob pb = make_prob(phys, cfg);
+    hipLaunchKernelGGL(k_AB, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, (hipStream_t)stream, pb, B, rho, A,
+                       Bv);
+    return check_hip(ctx, hipGetLastError(), "k_AB");
+}
+
+#define NTM_GROUP_LAUNCH(KERN, N, B, st, ...)                                                        \
+    do {                                                                                            \
+        int P_ = lanes_for(N);                                                                      \
+        int G_ = 64 / P_;                                                                           \
+        size_t lds_ = (size_t)G_ * ws_bytes(N);                                                     \
+        unsigned blocks_ = (unsigned)(((B) + G_ - 1) / G_);                                         \
+        if (P_ == 16) {                                                                             \
+            if ((rc = set_lds(ctx, KERN<16>, lds_))) return rc;                                     \
+            hipLaunchKernelGGL(KERN<16>, dim3(blocks_), dim3(64), lds_, st, __VA_ARGS__);           \
+        } else if (P_ == 32) {                                                                      \
+            if ((rc = set_lds(ctx, KERN<32>, lds_))) return rc;                                     \
+            hipLaunchKernelGGL(KERN<32>, dim3(blocks_), dim3(64), lds_, st, __VA_ARGS__);           \
+        } else {                                                                                    \
+            if ((rc = set_lds(ctx, KERN<64>, lds_))) return rc;                                     \
+            hipLaunchKernelGGL(KERN<64>, dim3(blocks_), dim3(64), lds_, st, __VA_ARGS__);           \
+        }                                                                                           \
+    } while (0)
+
+int ntm_lift_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* rho,
+                    double* Phi, double* Gamma, double* Lambda, void* stream) {
+    int rc = validate(ctx, phys, cfg, B);
+    if (rc || B == 0) return rc;
+    Prob pb = make_prob(phys, cfg);
+    NTM_GROUP_LAUNCH(k_lift, cfg->N, B, (hipStream_t)stream, pb, B, rho, Phi, Gamma, Lambda);
+    return check_hip(ctx, hipGetLastError(), "k_lift");
+}
+
+int ntm_cost_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* rho,
+                    const double* x_k, double* G, double* F, void* stream) {
+    int rc = validate(ctx, phys, cfg, B);
+    if (rc || B == 0) return rc;
+    Prob pb = make_prob(phys, cfg);
+    NTM_GROUP_LAUNCH(k_cost, cfg->N, B, (hipStream_t)stream, pb, B, rho, x_k, G, F);
+    return check_hip(ctx, hipGetLastError(), "k_cost");
+}
+
+int ntm_getwlc_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* rho,
+                      double* W, double* L, double* c, void* stream) {
+    int rc = validate(ctx, phys, cfg, B);
+    if (rc || B == 0) return rc;
+    Prob pb = make_prob(phys, cfg);
+    NTM_GROUP_LAUNCH(k_getwlc, cfg->N, B, (hipStream_t)stream, pb, B, rho, W, L, c);
+    return check_hip(ctx, hipGetLastError(), "k_getwlc");
+}
+
+int ntm_qp_device(ntm_ctx* ctx, int64_t B, int32_t N, int32_t m, const double* G, const double* F,
+                  const double* Lin, const double* b, double* U, int32_t* exitflag, int32_t* iters, void* stream) {
+    if (!ctx) return NTM_E_INVALID;
+    if (N < 1 || N > NTM_MAX_N) return fail(ctx, NTM_E_INVALID, "N out of range [1, 64]");
+    if (m < 0 || m > 6 * NTM_MAX_N + 4) return fail(ctx, NTM_E_INVALID, "m out of range");
+    if (B < 0) return fail(ctx, NTM_E_INVALID, "negative batch");
+    if (B == 0) return NTM_OK;
+    int P = lanes_for(N), Gs = 64 / P;
+    size_t per = (size_t)ws_bytes(N) + ((m * 8 + 15) & ~15);
+    size_t lds = Gs * per;
+    unsigned blocks = (unsigned)((B + Gs - 1) / Gs);
+    hipStream_t st = (hipStream_t)stream;
+    int rc;
+    if (P == 16) {
+        if ((rc = set_lds(ctx, k_qp<16>, lds))) return rc;
+        hipLaunchKernelGGL(k_qp<16>, dim3(blocks), dim3(64), lds, st, B, N, m, G, F, Lin, b, U, exitflag, iters);
+    } else if (P == 32) {
+        if ((rc = set_lds(ctx, k_qp<32>, lds))) return rc;
+        hipLaunchKernelGGL(k_qp<32>, dim3(blocks), dim3(64), lds, st, B, N, m, G, F, Lin, b, U, exitflag, iters);
+    } else {
+        if ((rc = set_lds(ctx, k_qp<64>, lds))) return rc;
+        hipLaunchKernelGGL(k_qp<64>, dim3(blocks), dim3(64), lds, st, B, N, m, G, F, Lin, b, U, exitflag, iters);
+    }
+    return check_hip(ctx, hipGetLastError(), "k_qp");
+}
+
+// splitmix64-based counter generator (identical to oracle/ntm_oracle.py scenario_x0)
+static uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+void ntm_scenarios_x0(uint64_t seed, int64_t first_id, int64_t B, double* x0) {
+    const double pi = 3.14159265358979323846;
+    for (int64_t k = 0; k < B; ++k) {
+        uint64_t sid = (uint64_t)(first_id + k);
+        uint64_t base = seed * 0x100000001B3ull + sid * 2;
+        double u0 = (double)(splitmix64(base) >> 11) * (1.0 / 9007199254740992.0);
+        double u1 = (double)(splitmix64(base + 1) >> 11) * (1.0 / 9007199254740992.0);
+        x0[k] = 0.07 + 0.07 * u0;
+        x0[B + k] = (0.8 + 0.4 * u1) * 2000 * pi;
+    }
+}
+
+}  // extern "C"

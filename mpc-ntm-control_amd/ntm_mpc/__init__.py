@@ -1,0 +1,14 @@
+"""ntm_mpc — MI355X-native batched LPV-MPC for NTM control (hot path of
+IsaacSavona/MPC-NTM-Control's NTM_MPC_Sim.m receding-horizon loop).
+
+Import requires nothing but the built HIP library at
+``mpc-ntm-control_amd/lib/libntm_mpc.so``; see ``api.py``.
+"""
+from ._lib import (EXIT_INFEASIBLE, EXIT_MAXITER, EXIT_NONFINITE, EXIT_OPTIMAL, LIB_PATH, MODE_BOX,
+                   MODE_FULL, MODE_NONE, NtmLibraryError, load)
+from .api import (Config, NtmMpc, NTM_MPC_Sim, Physics, Rho_to_PhiGammaLambda, quadprog, rho1, rho2, rho3,
+                  scenarios_x0)
+
+__all__ = ["Config", "NtmMpc", "NTM_MPC_Sim", "Physics", "Rho_to_PhiGammaLambda", "quadprog", "rho1", "rho2",
+           "rho3", "scenarios_x0", "load", "LIB_PATH", "NtmLibraryError", "MODE_NONE", "MODE_BOX", "MODE_FULL",
+           "EXIT_OPTIMAL", "EXIT_MAXITER", "EXIT_INFEASIBLE", "EXIT_NONFINITE"]

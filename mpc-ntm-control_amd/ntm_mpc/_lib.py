@@ -1,0 +1,106 @@
+"""ctypes binding of the C-ABI in include/ntm_mpc.h (lib/libntm_mpc.so).
+
+The product path has no fallback: if the HIP library is missing or fails to
+load, every call raises ``NtmLibraryError``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG_ROOT = Path(__file__).resolve().parent.parent          # mpc-ntm-control_amd/
+LIB_PATH = Path(os.environ.get("NTM_MPC_LIB", PKG_ROOT / "lib" / "libntm_mpc.so"))
+
+MAX_N = 64
+MODE_NONE, MODE_BOX, MODE_FULL = 0, 1, 2
+LITERAL_PHI_RIGHTMUL, LITERAL_GAMMA_INDEX, LITERAL_PLANT_NO_C, RHO1_SQUARED = 1, 2, 4, 8
+EXIT_OPTIMAL, EXIT_MAXITER, EXIT_INFEASIBLE, EXIT_NONFINITE = 1, 0, -2, -7
+NTM_OK = 0
+
+PHYSICS_FIELDS = ("j_BS w_dep w_marg w_sat tau_r rs a eta_CD tau_E0 tau_E mu0 Lq B_pol m Cw "
+                  "tau_A0 tau_w omega0").split()
+
+
+class NtmLibraryError(RuntimeError):
+    pass
+
+
+class NtmPhysics(C.Structure):
+    """ntm_physics — NTM_MPC_Sim.m:5-22."""
+    _fields_ = [(n, C.c_double) for n in PHYSICS_FIELDS]
+
+
+class NtmConfig(C.Structure):
+    """ntm_config — NTM_MPC_Sim.m:30-60, 80-88."""
+    _fields_ = [("N", C.c_int32), ("i_sim", C.c_int32), ("mode", C.c_int32), ("flags", C.c_int32),
+                ("Ts", C.c_double), ("xmin", C.c_double * 2), ("xmax", C.c_double * 2),
+                ("umin", C.c_double), ("umax", C.c_double), ("Q", C.c_double * 4),
+                ("r", C.c_double * 2), ("epsilon", C.c_double)]
+
+
+_DP = C.POINTER(C.c_double)
+_IP = C.POINTER(C.c_int32)
+_V = C.c_void_p
+_PHY = C.POINTER(NtmPhysics)
+_CFG = C.POINTER(NtmConfig)
+
+# name -> (restype, argtypes)
+EXPORTS = {
+    "ntm_physics_default": (None, [_PHY]),
+    "ntm_config_default": (None, [_CFG, C.c_int32]),
+    "ntm_abi_version": (C.c_int32, []),
+    "ntm_ctx_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32]),
+    "ntm_ctx_destroy": (None, [C.c_void_p]),
+    "ntm_last_error": (C.c_char_p, [C.c_void_p]),
+    "ntm_mpc_step": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _DP, _DP, _DP, _DP, _DP, _DP, _IP, _IP]),
+    "ntm_mpc_step_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
+    "ntm_mpc_run": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, C.c_int32, _DP, _DP, _DP, _DP, _DP, _IP, _IP]),
+    "ntm_mpc_run_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, C.c_int32, _V, _V, _V, _V, _V, _V,
+                                     _V, _V]),
+    "ntm_rho_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _V, _V, _V]),
+    "ntm_AB_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _V, _V, _V, _V]),
+    "ntm_lift_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _V, _V, _V, _V, _V]),
+    "ntm_cost_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _V, _V, _V, _V, _V]),
+    "ntm_getwlc_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _V, _V, _V, _V, _V]),
+    "ntm_qp_device": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, _V, _V, _V, _V, _V, _V, _V, _V]),
+    "ntm_scenarios_x0": (None, [C.c_uint64, C.c_int64, C.c_int64, _DP]),
+}
+
+_lib = None
+
+
+def load(path: Path | str | None = None):
+    """Load libntm_mpc.so (once) and bind every exported symbol."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path is not None else LIB_PATH
+    if not p.exists():
+        raise NtmLibraryError(f"HIP library not built: {p} (run `make -C mpc-ntm-control_amd` "
+                              "or __graft_entry__.build())")
+    try:
+        lib = C.CDLL(str(p))
+    except OSError as e:  # pragma: no cover - depends on the loader
+        raise NtmLibraryError(f"cannot load {p}: {e}") from e
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.ntm_abi_version() != 1:
+        raise NtmLibraryError("ABI version mismatch")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def default_physics() -> NtmPhysics:
+    p = NtmPhysics()
+    load().ntm_physics_default(C.byref(p))
+    return p
+
+
+def default_config(N: int) -> NtmConfig:
+    c = NtmConfig()
+    load().ntm_config_default(C.byref(c), N)
+    return c

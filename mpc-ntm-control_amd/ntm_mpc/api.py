@@ -1,0 +1,315 @@
+"""Host-side mirror of the reference's MATLAB interface over the HIP C-ABI.
+
+The reference (IsaacSavona/MPC-NTM-Control) is a MATLAB script whose hot path
+is a handful of functions resolved by name.  MATLAB is not available in this
+image, so the host side is Python; it keeps the reference's names, argument
+meaning and error behaviour, batched over scenarios:
+
+    rho1 / rho2 / rho3          rho1.m, rho2.m, rho3.m
+    A / B                       A.m, B.m
+    Rho_to_PhiGammaLambda       Rho_to_PhiGammaLambda.m
+    cost (G, F)                 NTM_MPC_Sim.m:120-121
+    getWLc                      getWLc.m
+    quadprog                    NTM_MPC_Sim.m:97 (exitflag semantics :98-103)
+    NtmMpc.step                 NTM_MPC_Sim.m:94-130  (one time step, drop-in)
+    NtmMpc.run / NTM_MPC_Sim    NTM_MPC_Sim.m:80-131  (closed loop)
+
+All batched tensors are torch fp64 CUDA tensors of shape (E, B) — element e
+of scenario s at [e, s], i.e. the C-ABI's scenario-minor SoA layout.  PyTorch
+is only plumbing (device memory, streams); every computation runs in the HIP
+kernels of lib/libntm_mpc.so.  There is no CPU fallback: without the library
+or a GPU, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib as L
+from ._lib import NtmConfig, NtmLibraryError, NtmPhysics
+
+
+@dataclass
+class Physics:
+    """Physics constants, NTM_MPC_Sim.m:5-22."""
+    j_BS: float = 73e3
+    w_dep: float = 0.024
+    w_marg: float = 0.02
+    w_sat: float = 0.32
+    tau_r: float = 293.0
+    rs: float = 1.55
+    a: float = 2.0
+    eta_CD: float = 0.9
+    tau_E0: float = 3.7
+    tau_E: float = 3.7
+    mu0: float = 4e-7 * math.pi
+    Lq: float = 0.87
+    B_pol: float = 0.97
+    m: float = 2.0
+    Cw: float = 1.0
+    tau_A0: float = 3e-6
+    tau_w: float = 0.188
+    omega0: float = 2 * math.pi * 420
+
+    def to_c(self) -> NtmPhysics:
+        return NtmPhysics(*[float(getattr(self, n)) for n in L.PHYSICS_FIELDS])
+
+
+@dataclass
+class Config:
+    """Controller configuration, NTM_MPC_Sim.m:30-60, 80-88 (mode/flags: SURVEY.md §2.1)."""
+    N: int = 20
+    Ts: float = 0.1
+    xmin: tuple = (0.06, 100 * 2 * math.pi)
+    xmax: tuple = (0.15, 5000 * 2 * math.pi)
+    umin: float = 0.0
+    umax: float = 2e6
+    Q: tuple = (1.0, 0.0, 0.0, 1.0)
+    r: tuple = (0.0, 1000 * 2 * math.pi)
+    i_sim: int = 10
+    epsilon: float = 1e-14
+    mode: int = L.MODE_FULL
+    flags: int = 0
+
+    def to_c(self) -> NtmConfig:
+        return NtmConfig(int(self.N), int(self.i_sim), int(self.mode), int(self.flags), float(self.Ts),
+                         (C.c_double * 2)(*self.xmin), (C.c_double * 2)(*self.xmax), float(self.umin),
+                         float(self.umax), (C.c_double * 4)(*self.Q), (C.c_double * 2)(*self.r),
+                         float(self.epsilon))
+
+    @property
+    def m(self) -> int:
+        return 0 if self.mode == L.MODE_NONE else (2 * self.N if self.mode == L.MODE_BOX else 6 * self.N + 4)
+
+
+def _ptr(t: torch.Tensor | None):
+    if t is None:
+        return None
+    return C.c_void_p(t.data_ptr())
+
+
+def _check_dev(t: torch.Tensor, shape, dtype=torch.float64, name="tensor"):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ValueError(f"{name} must be a CUDA tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+class NtmMpc:
+    """Batched LPV-MPC controller on one MI355X (one ``ntm_ctx`` per device)."""
+
+    def __init__(self, physics: Physics | None = None, config: Config | None = None, device: int | None = None):
+        self.lib = L.load()
+        if not torch.cuda.is_available():
+            raise NtmLibraryError("no GPU visible: the HIP path has no CPU fallback")
+        self.device = torch.cuda.current_device() if device is None else int(device)
+        self.physics = physics or Physics()
+        self.config = config or Config()
+        self._ctx = C.c_void_p()
+        rc = self.lib.ntm_ctx_create(C.byref(self._ctx), self.device)
+        if rc != L.NTM_OK:
+            raise NtmLibraryError(f"ntm_ctx_create failed ({rc})")
+
+    def close(self):
+        if self._ctx:
+            self.lib.ntm_ctx_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ helpers
+    def _cfg(self, cfg: Config | None):
+        return (cfg or self.config).to_c()
+
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _raise(self, rc, what):
+        if rc != L.NTM_OK:
+            raise NtmLibraryError(f"{what} failed ({rc}): {self.lib.ntm_last_error(self._ctx).decode()}")
+
+    def _empty(self, *shape, dtype=torch.float64):
+        return torch.empty(*shape, dtype=dtype, device=f"cuda:{self.device}")
+
+    # ------------------------------------------------------------ hot path
+    def initial_state(self, x0: torch.Tensor, cfg: Config | None = None):
+        """Rho = repmat(rho(x0), 1, N) (NTM_MPC_Sim.m:63-65); U_old = +inf (D14)."""
+        cfg = cfg or self.config
+        Bn = x0.shape[1]
+        r = self.rho(x0, cfg)                                   # (3, B)
+        rho = r.repeat(cfg.N, 1).contiguous()                   # (3N, B): element 3i + k
+        U_old = torch.full((cfg.N, Bn), float("inf"), dtype=torch.float64, device=x0.device)
+        return rho, U_old
+
+    def step(self, x_k: torch.Tensor, rho: torch.Tensor, U_old: torch.Tensor, cfg: Config | None = None,
+             out: dict | None = None):
+        """One MPC time step for a batch (NTM_MPC_Sim.m:94-130).  ``rho`` (3N, B) and
+        ``U_old`` (N, B) are updated in place.  Returns dict U, x_pred, x_next,
+        exitflag, inner_iters (all CUDA tensors)."""
+        cfg = cfg or self.config
+        N, Bn = cfg.N, x_k.shape[1]
+        _check_dev(x_k, (2, Bn), name="x_k")
+        _check_dev(rho, (3 * N, Bn), name="rho")
+        _check_dev(U_old, (N, Bn), name="U_old")
+        if out is None:
+            out = {"U": self._empty(N, Bn), "x_pred": self._empty(2 * (N + 1), Bn), "x_next": self._empty(2, Bn),
+                   "exitflag": self._empty(Bn, dtype=torch.int32), "inner_iters": self._empty(Bn, dtype=torch.int32)}
+        rc = self.lib.ntm_mpc_step_device(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn,
+                                          _ptr(x_k), _ptr(rho), _ptr(U_old), _ptr(out["U"]), _ptr(out["x_pred"]),
+                                          _ptr(out["x_next"]), _ptr(out["exitflag"]), _ptr(out["inner_iters"]),
+                                          self._stream())
+        self._raise(rc, "ntm_mpc_step_device")
+        return out
+
+    def run(self, x0: torch.Tensor, k_sim: int = 20, cfg: Config | None = None):
+        """Closed loop NTM_MPC_Sim.m:80-131 on device.  Returns the workspace
+        variables xk (2(k_sim+1), B), uk (k_sim, B), Uk (N k_sim, B), wpred
+        ((N+1) k_sim, B), exitflag / inner_iters (k_sim, B)."""
+        cfg = cfg or self.config
+        N, Bn = cfg.N, x0.shape[1]
+        _check_dev(x0, (2, Bn), name="x0")
+        out = {"xk": self._empty(2 * (k_sim + 1), Bn), "uk": self._empty(k_sim, Bn), "Uk": self._empty(N * k_sim, Bn),
+               "wpred": self._empty((N + 1) * k_sim, Bn), "exitflag": self._empty(k_sim, Bn, dtype=torch.int32),
+               "inner_iters": self._empty(k_sim, Bn, dtype=torch.int32)}
+        rc = self.lib.ntm_mpc_run_device(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn, k_sim,
+                                         _ptr(x0), _ptr(out["xk"]), _ptr(out["uk"]), _ptr(out["Uk"]),
+                                         _ptr(out["wpred"]), _ptr(out["exitflag"]), _ptr(out["inner_iters"]),
+                                         self._stream())
+        self._raise(rc, "ntm_mpc_run_device")
+        return out
+
+    # ------------------------------------------------------------ function level
+    def rho(self, x: torch.Tensor, cfg: Config | None = None):
+        """rho1.m / rho2.m / rho3.m at x (2, B) -> (3, B)."""
+        Bn = x.shape[1]
+        _check_dev(x, (2, Bn), name="x")
+        out = self._empty(3, Bn)
+        self._raise(self.lib.ntm_rho_device(self._ctx, C.byref(self.physics.to_c()), C.byref(self._cfg(cfg)), Bn,
+                                            _ptr(x), _ptr(out), self._stream()), "ntm_rho_device")
+        return out
+
+    def AB(self, rho: torch.Tensor, cfg: Config | None = None):
+        """A.m / B.m at rho (3, B) -> A (4, B) col-major 2x2, B (2, B) column (D5)."""
+        Bn = rho.shape[1]
+        _check_dev(rho, (3, Bn), name="rho")
+        A, Bv = self._empty(4, Bn), self._empty(2, Bn)
+        self._raise(self.lib.ntm_AB_device(self._ctx, C.byref(self.physics.to_c()), C.byref(self._cfg(cfg)), Bn,
+                                           _ptr(rho), _ptr(A), _ptr(Bv), self._stream()), "ntm_AB_device")
+        return A, Bv
+
+    def lift(self, rho: torch.Tensor, cfg: Config | None = None):
+        """Rho_to_PhiGammaLambda.m: rho (3N, B) -> Phi (4N, B), Gamma (2N*N, B), Lambda (2N, B)."""
+        cfg = cfg or self.config
+        N, Bn = cfg.N, rho.shape[1]
+        _check_dev(rho, (3 * N, Bn), name="rho")
+        Phi, Gam, Lam = self._empty(4 * N, Bn), self._empty(2 * N * N, Bn), self._empty(2 * N, Bn)
+        self._raise(self.lib.ntm_lift_device(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn,
+                                             _ptr(rho), _ptr(Phi), _ptr(Gam), _ptr(Lam), self._stream()),
+                    "ntm_lift_device")
+        return Phi, Gam, Lam
+
+    def cost(self, rho: torch.Tensor, x_k: torch.Tensor, cfg: Config | None = None):
+        """NTM_MPC_Sim.m:120-121 -> G (N*N, B), F (N, B)."""
+        cfg = cfg or self.config
+        N, Bn = cfg.N, rho.shape[1]
+        _check_dev(rho, (3 * N, Bn), name="rho")
+        _check_dev(x_k, (2, Bn), name="x_k")
+        G, F = self._empty(N * N, Bn), self._empty(N, Bn)
+        self._raise(self.lib.ntm_cost_device(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn,
+                                             _ptr(rho), _ptr(x_k), _ptr(G), _ptr(F), self._stream()),
+                    "ntm_cost_device")
+        return G, F
+
+    def getWLc(self, rho: torch.Tensor, cfg: Config | None = None):
+        """getWLc.m -> W (2m, B), L (m*N, B), c (m, B), m = 6N+4 (column-major per scenario)."""
+        cfg = cfg or self.config
+        N, Bn = cfg.N, rho.shape[1]
+        m = 6 * N + 4
+        _check_dev(rho, (3 * N, Bn), name="rho")
+        W, Lm, c = self._empty(2 * m, Bn), self._empty(m * N, Bn), self._empty(m, Bn)
+        self._raise(self.lib.ntm_getwlc_device(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn,
+                                               _ptr(rho), _ptr(W), _ptr(Lm), _ptr(c), self._stream()),
+                    "ntm_getwlc_device")
+        return W, Lm, c
+
+    def quadprog(self, H: torch.Tensor, f: torch.Tensor, Lin: torch.Tensor | None, b: torch.Tensor | None):
+        """quadprog(H, f, A, b) for a batch: min 1/2 U'HU + f'U s.t. Lin U <= b.
+        H (N*N, B), f (N, B), Lin (m*N, B) column-major per scenario, b (m, B).
+        Returns (U (N, B), exitflag (B,), iterations (B,)); exitflag as quadprog
+        (1 optimal, 0 max iterations, -2 infeasible -> U = 0, -7 non-finite)."""
+        N, Bn = f.shape
+        m = 0 if Lin is None else b.shape[0]
+        _check_dev(H, (N * N, Bn), name="H")
+        _check_dev(f, (N, Bn), name="f")
+        if m:
+            _check_dev(Lin, (m * N, Bn), name="A")
+            _check_dev(b, (m, Bn), name="b")
+        U = self._empty(N, Bn)
+        flag = self._empty(Bn, dtype=torch.int32)
+        its = self._empty(Bn, dtype=torch.int32)
+        self._raise(self.lib.ntm_qp_device(self._ctx, Bn, N, m, _ptr(H), _ptr(f), _ptr(Lin) if m else None,
+                                           _ptr(b) if m else None, _ptr(U), _ptr(flag), _ptr(its), self._stream()),
+                    "ntm_qp_device")
+        return U, flag, its
+
+
+def scenarios_x0(first_id: int, B: int, seed: int = 20241220):
+    """Synthetic initial states for global ids first_id..first_id+B-1, (2, B) float64 numpy."""
+    import numpy as np
+    x0 = np.empty((2, B), dtype=np.float64)
+    L.load().ntm_scenarios_x0(C.c_uint64(seed), first_id, B, x0.ctypes.data_as(C.POINTER(C.c_double)))
+    return x0
+
+
+# ---- MATLAB-named thin wrappers (reference function names) ----------------
+
+_default = None
+
+
+def _ctl():
+    global _default
+    if _default is None:
+        _default = NtmMpc()
+    return _default
+
+
+def rho1(x, w_marg=None):
+    """rho1.m (batched): x (2, B) CUDA -> (B,)."""
+    return _ctl().rho(x)[0]
+
+
+def rho2(x):
+    """rho2.m (batched)."""
+    return _ctl().rho(x)[1]
+
+
+def rho3(x, w_dep=None):
+    """rho3.m (batched)."""
+    return _ctl().rho(x)[2]
+
+
+def Rho_to_PhiGammaLambda(Rho1, Rho2, Rho3, cfg: Config | None = None):
+    """Rho_to_PhiGammaLambda.m (batched): Rho1/2/3 (N, B) -> Phi, Gamma, Lambda."""
+    rho = torch.stack([Rho1, Rho2, Rho3], dim=1).reshape(-1, Rho1.shape[1]).contiguous()
+    return _ctl().lift(rho, cfg)
+
+
+def quadprog(H, f, A=None, b=None):
+    """quadprog stand-in (NTM_MPC_Sim.m:97)."""
+    return _ctl().quadprog(H, f, A, b)
+
+
+def NTM_MPC_Sim(x0, k_sim: int = 20, cfg: Config | None = None):
+    """The driver NTM_MPC_Sim.m:80-131 for a batch of initial states x0 (2, B)."""
+    return _ctl().run(x0, k_sim, cfg)

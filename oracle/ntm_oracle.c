@@ -1,0 +1,553 @@
+/*
+ * ntm_oracle.c — C restatement of the CPU oracle.  TEST INFRASTRUCTURE ONLY.
+ *
+ * The checker, never the product: only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg load liboracle (oracle/libntm_oracle.so).  It is
+ * the C twin of oracle/ntm_oracle.py (same CANON semantics, SURVEY.md §2.1,
+ * same Goldfarb-Idnani QP) and is itself pinned against the Python oracle by
+ * tests/test_oracle_c.py; the Python oracle is pinned by the reference-derived
+ * invariants and 50-digit KKT certificates (see its header).  It is also the
+ * CPU baseline timed by bench.py ("kind": "port": the reference is MATLAB and
+ * cannot run here).  OpenMP parallelism is over independent scenarios.
+ *
+ * Reference citations (file:line of /root/reference):
+ *   rho1.m:2, rho2.m:2, rho3.m:2-3         -> orc_rho
+ *   A.m:2, B.m:2, NTM_MPC_Sim.m:24-25,37   -> orc_coeffs / orc_A / orc_B
+ *   Rho_to_PhiGammaLambda.m:17-52          -> orc_lift   (CANON D4, D6)
+ *   NTM_MPC_Sim.m:67-73,120-121            -> orc_cost   (CANON D8, D12)
+ *   getWLc.m:9-59                          -> orc_getwlc (CANON D10)
+ *   NTM_MPC_Sim.m:97 (quadprog)            -> orc_qp     (Goldfarb-Idnani)
+ *   NTM_MPC_Sim.m:110-117,123-127,130      -> orc_step
+ *   NTM_MPC_Sim.m:80-131                   -> ntm_oracle_run
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/ntm_mpc.h"
+
+#define NMAX NTM_MAX_N
+#define MMAX (6 * NMAX + 4)
+
+typedef struct {
+    double a11c, a21num_den, a22, bc, C1, C2, wmarg2, wdep;
+    int rho1_sq;
+} orc_coef;
+
+/* NTM_MPC_Sim.m:24-25 (kappa, zeta), A.m:2, B.m:2, :37 (C). */
+static void orc_coeffs(const ntm_physics* p, const ntm_config* c, orc_coef* k) {
+    const double pi = 3.14159265358979323846;
+    double kappa = 16 * p->mu0 * p->Lq * (p->rs * p->rs) / (0.82 * p->tau_r * p->B_pol * pi);
+    double zeta = p->m * p->Cw * (p->tau_A0 * p->tau_A0) * p->tau_w * (p->a * p->a * p->a);
+    double Ts = c->Ts;
+    k->a11c = (4.0 / 3.0) * (kappa * p->rs / (0.82 * p->tau_r)) * Ts;
+    k->a21num_den = zeta * (p->a * p->a * p->a);      /* (rho2*Ts)/(zeta*a^3), D19 */
+    k->a22 = 1 - Ts / p->tau_E;
+    k->bc = (kappa * Ts * p->eta_CD / p->w_dep);
+    k->C1 = -4.0 / 3.0 * (kappa * Ts * p->j_BS * p->w_sat) / (p->w_sat * p->w_sat + p->w_marg * p->w_marg);
+    k->C2 = Ts * p->omega0 / p->tau_E0;
+    k->wmarg2 = p->w_marg * p->w_marg;
+    k->wdep = p->w_dep;
+    k->rho1_sq = (c->flags & NTM_RHO1_SQUARED) != 0;
+}
+
+/* rho1.m:2, rho2.m:2, rho3.m:2-3 */
+static void orc_rho(const orc_coef* k, const double* x, double* r) {
+    double w = x[0];
+    r[0] = 1.0 / ((k->rho1_sq ? w * w : w) + k->wmarg2);
+    r[1] = (w * w) / x[1];
+    double ws = w / k->wdep;
+    r[2] = (0.25 + 0.24 * ws) / (1 + 1.5 * ws + 0.43 * (ws * ws) + 0.64 * (ws * ws * ws));
+}
+
+/* A.m:2 -> a11, a21 (a12 = 0, a22 constant) ; B.m:2 -> b (column [b;0], D5) */
+static inline double orc_a11(const orc_coef* k, double r1) { return k->a11c * r1 + 1; }
+static inline double orc_a21(const orc_coef* k, double r2, double Ts) { return (r2 * Ts) / k->a21num_den; }
+static inline double orc_b(const orc_coef* k, double r3) { return k->bc * r3; }
+
+/* Rho_to_PhiGammaLambda.m:1-54 (CANON D3-D6).  rho: 3xN col-major.
+ * Phi 2N x 2, Gamma 2N x N, Lambda 2N, all column-major. */
+static void orc_lift(const orc_coef* k, const ntm_config* c, const double* rho,
+                     double* Phi, double* Gam, double* Lam) {
+    int N = c->N, R = 2 * N;
+    double a11[NMAX], a21[NMAX], b[NMAX];
+    for (int i = 0; i < N; ++i) {
+        a11[i] = orc_a11(k, rho[3 * i]);
+        a21[i] = orc_a21(k, rho[3 * i + 1], c->Ts);
+        b[i] = orc_b(k, rho[3 * i + 2]);
+    }
+    double a22 = k->a22;
+    /* Phi (:17-23) */
+    Phi[0] = a11[0]; Phi[1] = a21[0]; Phi[R + 0] = 0.0; Phi[R + 1] = a22;
+    for (int j = 1; j < N; ++j) {
+        double p00 = Phi[2 * j - 2], p10 = Phi[2 * j - 1];
+        double p01 = Phi[R + 2 * j - 2], p11 = Phi[R + 2 * j - 1];
+        if (c->flags & NTM_LITERAL_PHI_RIGHTMUL) {        /* D4 literal: Phi_{j-1} A_j */
+            Phi[2 * j] = p00 * a11[j] + p01 * a21[j];
+            Phi[R + 2 * j] = p01 * a22;
+            Phi[2 * j + 1] = p10 * a11[j] + p11 * a21[j];
+            Phi[R + 2 * j + 1] = p11 * a22;
+        } else {                                         /* CANON: A_j Phi_{j-1} */
+            Phi[2 * j] = a11[j] * p00;
+            Phi[R + 2 * j] = a11[j] * p01;
+            Phi[2 * j + 1] = a21[j] * p00 + a22 * p10;
+            Phi[R + 2 * j + 1] = a21[j] * p01 + a22 * p11;
+        }
+    }
+    /* Gamma (:26-40) */
+    memset(Gam, 0, sizeof(double) * (size_t)R * N);
+    for (int j = 0; j < N; ++j) {
+        Gam[(size_t)j * R + 2 * j] = b[j];
+        Gam[(size_t)j * R + 2 * j + 1] = 0.0;
+    }
+    for (int i = 1; i < N; ++i) {
+        for (int j = 0; j < i; ++j) {
+            int ai = (c->flags & NTM_LITERAL_GAMMA_INDEX) ? (i - j - 1) : i;   /* D6 */
+            double g0 = Gam[(size_t)j * R + 2 * i - 2], g1 = Gam[(size_t)j * R + 2 * i - 1];
+            Gam[(size_t)j * R + 2 * i] = a11[ai] * g0;
+            Gam[(size_t)j * R + 2 * i + 1] = a21[ai] * g0 + a22 * g1;
+        }
+    }
+    /* Lambda (:47-52) */
+    Lam[0] = k->C1; Lam[1] = k->C2;
+    for (int i = 1; i < N; ++i) {
+        double l0 = Lam[2 * i - 2], l1 = Lam[2 * i - 1];
+        Lam[2 * i] = a11[i] * l0 + k->C1;
+        Lam[2 * i + 1] = (a21[i] * l0 + a22 * l1) + k->C2;
+    }
+}
+
+/* NTM_MPC_Sim.m:71-73,120-121: G = 2 Gam' Om Gam, F = 2 Gam' Om (Phi x + Lam - R). */
+static void orc_cost(const ntm_config* c, const double* Phi, const double* Gam,
+                     const double* Lam, const double* x, double* G, double* F) {
+    int N = c->N, R = 2 * N;
+    double q00 = c->Q[0], q01 = c->Q[1], q10 = c->Q[2], q11 = c->Q[3];
+    double OG[2 * NMAX * NMAX];  /* Om*Gam (2N x N) */
+    for (int j = 0; j < N; ++j)
+        for (int i = 0; i < N; ++i) {
+            double g0 = Gam[(size_t)j * R + 2 * i], g1 = Gam[(size_t)j * R + 2 * i + 1];
+            OG[(size_t)j * R + 2 * i] = q00 * g0 + q01 * g1;
+            OG[(size_t)j * R + 2 * i + 1] = q10 * g0 + q11 * g1;
+        }
+    for (int a = 0; a < N; ++a)
+        for (int b = 0; b < N; ++b) {
+            double s = 0.0;
+            for (int r = 0; r < R; ++r) s += Gam[(size_t)a * R + r] * OG[(size_t)b * R + r];
+            G[(size_t)b * N + a] = 2 * s;
+        }
+    double e[2 * NMAX];
+    for (int i = 0; i < N; ++i) {
+        e[2 * i] = (Phi[2 * i] * x[0] + Phi[R + 2 * i] * x[1]) + Lam[2 * i] - c->r[0];
+        e[2 * i + 1] = (Phi[2 * i + 1] * x[0] + Phi[R + 2 * i + 1] * x[1]) + Lam[2 * i + 1] - c->r[1];
+    }
+    for (int a = 0; a < N; ++a) {
+        double s = 0.0;
+        for (int i = 0; i < N; ++i) {
+            double oe0 = q00 * e[2 * i] + q01 * e[2 * i + 1];
+            double oe1 = q10 * e[2 * i] + q11 * e[2 * i + 1];
+            s += Gam[(size_t)a * R + 2 * i] * oe0 + Gam[(size_t)a * R + 2 * i + 1] * oe1;
+        }
+        F[a] = 2 * s;
+    }
+}
+
+/* getWLc.m:9-59 (D10 fix).  Row order per block i=0..N-1:
+ * [-u_i; u_i; -w_i; -om_i; w_i; om_i], terminal [-w_N; -om_N; w_N; om_N].
+ * W m x 2, L m x N, c m (column-major). */
+static void orc_getwlc(const ntm_config* c, const double* Phi, const double* Gam,
+                       const double* Lam, double* W, double* L, double* cv) {
+    int N = c->N, R = 2 * N, m = 6 * N + 4;
+    memset(W, 0, sizeof(double) * (size_t)m * 2);
+    memset(L, 0, sizeof(double) * (size_t)m * N);
+    for (int i = 0; i <= N; ++i) {
+        int base = 6 * i;
+        int xr = base + (i < N ? 2 : 0);   /* first state row of this block */
+        if (i < N) {
+            L[(size_t)i * m + base] = -1.0;            /* Ecal: -u_i */
+            L[(size_t)i * m + base + 1] = 1.0;         /*        u_i */
+            cv[base] = -c->umin;
+            cv[base + 1] = c->umax;
+        }
+        cv[xr] = -c->xmin[0]; cv[xr + 1] = -c->xmin[1];
+        cv[xr + 2] = c->xmax[0]; cv[xr + 3] = c->xmax[1];
+        if (i == 0) {                                   /* Dcal: W = -Mi */
+            W[xr] = 1.0; W[m + xr + 1] = 1.0;
+            W[xr + 2] = -1.0; W[m + xr + 3] = -1.0;
+            continue;
+        }
+        int sr = 2 * (i - 1);                           /* x_i rows of Phi/Gam/Lam */
+        for (int s = 0; s < 2; ++s) {
+            double sg = (s == 0) ? -1.0 : 1.0;          /* -x (min) then +x (max) */
+            for (int comp = 0; comp < 2; ++comp) {
+                int row = xr + 2 * s + comp;
+                for (int j = 0; j < N; ++j) L[(size_t)j * m + row] = sg * Gam[(size_t)j * R + sr + comp];
+                W[row] = -sg * Phi[sr + comp];
+                W[m + row] = -sg * Phi[R + sr + comp];
+                cv[row] -= sg * Lam[sr + comp];
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* Goldfarb-Idnani dual active set: min 1/2 U'GU + F'U  s.t. Lin U <= b. */
+/* ------------------------------------------------------------------ */
+static void givens(double a, double b, double* cc, double* ss, double* h) {
+    double hh = hypot(a, b);
+    if (hh == 0.0) { *cc = 1.0; *ss = 0.0; *h = 0.0; return; }
+    *cc = a / hh; *ss = b / hh; *h = hh;
+}
+
+static int orc_gi(int n, int m, const double* G, const double* F, const double* Lin,
+                  const double* b, double* U, int* iters_out) {
+    double J[NMAX * NMAX], Rm[NMAX * NMAX], Lc[NMAX * NMAX];
+    double up[NMAX + 1], d[NMAX], z[NMAX], r[NMAX];
+    static const int max_extra = 50;
+    int act[NMAX + 1];
+    int q = 0, it = 0, max_iter = 10 * (n + m) + max_extra;
+    *iters_out = 0;
+    for (int i = 0; i < n; ++i) U[i] = 0.0;
+    for (int i = 0; i < n * n; ++i) if (!isfinite(G[i])) return NTM_EXIT_NONFINITE;
+    for (int i = 0; i < n; ++i) if (!isfinite(F[i])) return NTM_EXIT_NONFINITE;
+    for (int i = 0; i < m * n; ++i) if (!isfinite(Lin[i])) return NTM_EXIT_NONFINITE;
+    for (int i = 0; i < m; ++i) if (!isfinite(b[i])) return NTM_EXIT_NONFINITE;
+    /* GI form n_i'U >= bc_i with n_i = -Lin_i, bc_i = -b_i; constant rows (D15). */
+    double nrm[MMAX];
+    unsigned char nz[MMAX];
+    for (int i = 0; i < m; ++i) {
+        double s = 0.0;
+        for (int j = 0; j < n; ++j) s += Lin[(size_t)j * m + i] * Lin[(size_t)j * m + i];
+        nrm[i] = sqrt(s);
+        nz[i] = s > 0.0;
+        if (!nz[i] && -b[i] > 0.0) return NTM_EXIT_INFEASIBLE;
+    }
+    /* Cholesky G = Lc Lc' (lower, row-major Lc[i*n+j]) */
+    for (int j = 0; j < n; ++j) {
+        double s = G[(size_t)j * n + j];
+        for (int k = 0; k < j; ++k) s -= Lc[j * n + k] * Lc[j * n + k];
+        if (!(s > 0.0)) return NTM_EXIT_NONFINITE;
+        double l = sqrt(s);
+        Lc[j * n + j] = l;
+        for (int i = j + 1; i < n; ++i) {
+            double t = G[(size_t)j * n + i];
+            for (int k = 0; k < j; ++k) t -= Lc[i * n + k] * Lc[j * n + k];
+            Lc[i * n + j] = t / l;
+        }
+        for (int i = 0; i < j; ++i) Lc[i * n + j] = 0.0;
+    }
+    /* J = Lc^{-T}: solve Lc X = I (X = Lc^{-1}, lower), J = X' (row-major J[i*n+k]) */
+    for (int col = 0; col < n; ++col) {
+        double x[NMAX];
+        for (int i = 0; i < n; ++i) {
+            double s = (i == col) ? 1.0 : 0.0;
+            for (int k = 0; k < i; ++k) s -= Lc[i * n + k] * x[k];
+            x[i] = s / Lc[i * n + i];
+        }
+        for (int i = 0; i < n; ++i) J[col * n + i] = x[i];   /* J[col][i] = X[i][col] */
+    }
+    memset(Rm, 0, sizeof(double) * (size_t)n * n);
+    /* U = -J J' F */
+    {
+        double t[NMAX];
+        for (int k = 0; k < n; ++k) { double s = 0.0; for (int i = 0; i < n; ++i) s += J[i * n + k] * F[i]; t[k] = s; }
+        for (int i = 0; i < n; ++i) { double s = 0.0; for (int k = 0; k < n; ++k) s += J[i * n + k] * t[k]; U[i] = -s; }
+    }
+    for (;;) {
+        /* choose the most violated (normalised) inactive row */
+        int p = -1; double best = 0.0, sp_best = 0.0;
+        double umax_abs = 1.0;
+        for (int j = 0; j < n; ++j) if (fabs(U[j]) > umax_abs) umax_abs = fabs(U[j]);
+        for (int i = 0; i < m; ++i) {
+            if (!nz[i]) continue;
+            int isact = 0;
+            for (int a = 0; a < q; ++a) if (act[a] == i) { isact = 1; break; }
+            if (isact) continue;
+            double s = 0.0;
+            for (int j = 0; j < n; ++j) s -= Lin[(size_t)j * m + i] * U[j];
+            s += b[i];                                    /* s = n_i'U - bc_i */
+            double v = s / nrm[i];
+            if (p < 0 || v < best) { best = v; p = i; sp_best = s; }
+        }
+        if (p < 0) { *iters_out = it; return NTM_EXIT_OPTIMAL; }
+        double tolp = 1e-12 * fmax(nrm[p] * umax_abs, fabs(b[p]));
+        if (sp_best >= -tolp) { *iters_out = it; return NTM_EXIT_OPTIMAL; }
+        double np_[NMAX];
+        for (int j = 0; j < n; ++j) np_[j] = -Lin[(size_t)j * m + p];
+        up[q] = 0.0;
+        for (;;) {
+            if (++it > max_iter) { *iters_out = it; return NTM_EXIT_MAXITER; }
+            for (int k = 0; k < n; ++k) { double s = 0.0; for (int i = 0; i < n; ++i) s += J[i * n + k] * np_[i]; d[k] = s; }
+            double znrm = 0.0, dnrm = 0.0;
+            for (int i = 0; i < n; ++i) {
+                double s = 0.0;
+                for (int k = q; k < n; ++k) s += J[i * n + k] * d[k];
+                z[i] = s; znrm += s * s;
+            }
+            for (int k = 0; k < n; ++k) dnrm += d[k] * d[k];
+            for (int a = q - 1; a >= 0; --a) {            /* r = R^{-1} d[0:q] */
+                double s = d[a];
+                for (int bb = a + 1; bb < q; ++bb) s -= Rm[a * n + bb] * r[bb];
+                r[a] = s / Rm[a * n + a];
+            }
+            double t1 = INFINITY; int l = -1;
+            for (int a = 0; a < q; ++a)
+                if (r[a] > 0.0) { double ta = up[a] / r[a]; if (ta < t1) { t1 = ta; l = a; } }
+            double zn = 0.0, sp = b[p];                   /* sp = n_p'U - bc_p */
+            for (int j = 0; j < n; ++j) { zn += z[j] * np_[j]; sp += np_[j] * U[j]; }
+            double t2 = (fabs(zn) <= 1e-300 || sqrt(znrm) <= 1e-14 * sqrt(dnrm)) ? INFINITY : -sp / zn;
+            double t = t1 < t2 ? t1 : t2;
+            if (t == INFINITY) { for (int j = 0; j < n; ++j) U[j] = 0.0; *iters_out = it; return NTM_EXIT_INFEASIBLE; }
+            if (t2 == INFINITY) {
+                for (int a = 0; a < q; ++a) up[a] -= t * r[a];
+                up[q] += t;
+            } else {
+                for (int j = 0; j < n; ++j) U[j] += t * z[j];
+                for (int a = 0; a < q; ++a) up[a] -= t * r[a];
+                up[q] += t;
+                if (t == t2) {                                 /* add constraint p */
+                    for (int kk = n - 1; kk > q; --kk) {
+                        double cc, ss, h;
+                        givens(d[kk - 1], d[kk], &cc, &ss, &h);
+                        d[kk - 1] = h; d[kk] = 0.0;
+                        for (int i = 0; i < n; ++i) {
+                            double j1 = J[i * n + kk - 1], j2 = J[i * n + kk];
+                            J[i * n + kk - 1] = cc * j1 + ss * j2;
+                            J[i * n + kk] = -ss * j1 + cc * j2;
+                        }
+                    }
+                    for (int a = 0; a <= q; ++a) Rm[a * n + q] = d[a];
+                    act[q] = p;
+                    ++q;
+                    break;
+                }
+            }
+            /* drop constraint l (partial step, or dual-only step) */
+            for (int a = 0; a < n; ++a)
+                for (int bb = l; bb < q - 1; ++bb) Rm[a * n + bb] = Rm[a * n + bb + 1];
+            for (int a = 0; a < n; ++a) Rm[a * n + q - 1] = 0.0;
+            for (int jj = l; jj < q - 1; ++jj) {
+                double cc, ss, h;
+                givens(Rm[jj * n + jj], Rm[(jj + 1) * n + jj], &cc, &ss, &h);
+                for (int bb = jj; bb < n; ++bb) {
+                    double r1 = Rm[jj * n + bb], r2 = Rm[(jj + 1) * n + bb];
+                    Rm[jj * n + bb] = cc * r1 + ss * r2;
+                    Rm[(jj + 1) * n + bb] = -ss * r1 + cc * r2;
+                }
+                Rm[(jj + 1) * n + jj] = 0.0;
+                for (int i = 0; i < n; ++i) {
+                    double j1 = J[i * n + jj], j2 = J[i * n + jj + 1];
+                    J[i * n + jj] = cc * j1 + ss * j2;
+                    J[i * n + jj + 1] = -ss * j1 + cc * j2;
+                }
+            }
+            for (int a = l; a < q; ++a) { act[a] = act[a + 1]; up[a] = up[a + 1]; }
+            --q;
+        }
+    }
+}
+
+/* quadprog stand-in: Jacobi variable scaling U = D V (diag(DGD) = 1) and
+ * unit-norm constraint rows, then Goldfarb-Idnani on the scaled problem
+ * (cond(G) ~1e9-1e11 drops to ~1e6; see oracle/ntm_oracle.py qp_solve). */
+static int orc_qp(int n, int m, const double* G, const double* F, const double* Lin,
+                  const double* b, double* U, int* iters_out) {
+    static __thread double Gs[NMAX * NMAX], Ls[MMAX * NMAX];
+    double D[NMAX], Fs[NMAX], bs[MMAX], V[NMAX];
+    for (int j = 0; j < n; ++j) {
+        double g = G[(size_t)j * n + j];
+        D[j] = (g > 0.0) ? 1.0 / sqrt(g) : 1.0;
+    }
+    for (int j = 0; j < n; ++j) {
+        for (int i = 0; i < n; ++i) Gs[(size_t)j * n + i] = G[(size_t)j * n + i] * D[i] * D[j];
+        Fs[j] = F[j] * D[j];
+    }
+    for (int i = 0; i < m; ++i) {
+        double s = 0.0;
+        for (int j = 0; j < n; ++j) { double v = Lin[(size_t)j * m + i] * D[j]; Ls[(size_t)j * m + i] = v; s += v * v; }
+        double rn = s > 0.0 ? sqrt(s) : 1.0;
+        for (int j = 0; j < n; ++j) Ls[(size_t)j * m + i] /= rn;
+        bs[i] = b[i] / rn;
+    }
+    int flag = orc_gi(n, m, Gs, Fs, Ls, bs, V, iters_out);
+    for (int j = 0; j < n; ++j) U[j] = V[j] * D[j];
+    return flag;
+}
+
+/* Solve the configured QP for one scenario; returns exitflag. */
+static int orc_solve(const orc_coef* k, const ntm_config* c, const double* rho,
+                     const double* x, double* U, int* qp_iters) {
+    int N = c->N, R = 2 * N;
+    double Phi[2 * NMAX * 2], Gam[2 * NMAX * NMAX], Lam[2 * NMAX];
+    double G[NMAX * NMAX], F[NMAX];
+    (void)R;
+    orc_lift(k, c, rho, Phi, Gam, Lam);
+    orc_cost(c, Phi, Gam, Lam, x, G, F);
+    *qp_iters = 0;
+    if (c->mode == NTM_MODE_NONE) {
+        int flag = orc_qp(N, 0, G, F, NULL, NULL, U, qp_iters);
+        return flag;
+    }
+    if (c->mode == NTM_MODE_BOX) {
+        double Lin[2 * NMAX * NMAX], bb[2 * NMAX];
+        memset(Lin, 0, sizeof(double) * (size_t)2 * N * N);
+        for (int j = 0; j < N; ++j) {
+            Lin[(size_t)j * 2 * N + j] = -1.0;
+            Lin[(size_t)j * 2 * N + N + j] = 1.0;
+            bb[j] = -c->umin;
+            bb[N + j] = c->umax;
+        }
+        return orc_qp(N, 2 * N, G, F, Lin, bb, U, qp_iters);
+    }
+    int m = 6 * N + 4;
+    double W[MMAX * 2], L[MMAX * NMAX], cv[MMAX];
+    orc_getwlc(c, Phi, Gam, Lam, W, L, cv);
+    for (int i = 0; i < m; ++i) cv[i] += W[i] * x[0] + W[m + i] * x[1];   /* c + W x_k (:97) */
+    return orc_qp(N, m, G, F, L, cv, U, qp_iters);
+}
+
+/* One MPC step, NTM_MPC_Sim.m:94-130 (CANON ordering). */
+static void orc_step(const orc_coef* k, const ntm_config* c, const double* x,
+                     double* rho, double* Uold, double* U, double* xpred,
+                     double* xnext, int* flag_out, int* iters_out) {
+    int N = c->N;
+    int flag = NTM_EXIT_OPTIMAL, it = 0;
+    for (it = 1; it <= c->i_sim; ++it) {
+        int qi;
+        flag = orc_solve(k, c, rho, x, U, &qi);
+        /* rollout + rho update (:110-117) */
+        double x0 = x[0], x1 = x[1];
+        xpred[0] = x0; xpred[1] = x1;
+        for (int i = 0; i < N; ++i) {
+            double a11 = orc_a11(k, rho[3 * i]);
+            double a21 = orc_a21(k, rho[3 * i + 1], c->Ts);
+            double b = orc_b(k, rho[3 * i + 2]);
+            double n0 = (a11 * x0 + b * U[i]) + k->C1;
+            double n1 = (a21 * x0 + k->a22 * x1) + k->C2;
+            double xi[2] = {x0, x1};
+            orc_rho(k, xi, &rho[3 * i]);
+            x0 = n0; x1 = n1;
+            xpred[2 * i + 2] = x0; xpred[2 * i + 3] = x1;
+        }
+        double s = 0.0;                                      /* :123 */
+        for (int j = 0; j < N; ++j) s += fabs(Uold[j] - U[j]);
+        for (int j = 0; j < N; ++j) Uold[j] = U[j];          /* :127 */
+        if (s < c->epsilon) break;
+    }
+    if (it > c->i_sim) it = c->i_sim;
+    /* plant step (:130, D13) */
+    double r[3];
+    orc_rho(k, x, r);
+    double a11 = orc_a11(k, r[0]), a21 = orc_a21(k, r[1], c->Ts), b = orc_b(k, r[2]);
+    xnext[0] = a11 * x[0] + b * U[0];
+    xnext[1] = a21 * x[0] + k->a22 * x[1];
+    if (!(c->flags & NTM_LITERAL_PLANT_NO_C)) { xnext[0] += k->C1; xnext[1] += k->C2; }
+    *flag_out = flag;
+    *iters_out = it;
+}
+
+/* ------------------------------------------------------------------ */
+/* exported (ctypes) entry points                                     */
+/* ------------------------------------------------------------------ */
+#define EXPORT __attribute__((visibility("default")))
+
+static int valid(const ntm_config* c) {
+    return c && c->N >= 1 && c->N <= NMAX && c->i_sim >= 1 && c->mode >= 0 && c->mode <= 2;
+}
+
+EXPORT int ntm_oracle_rho(const ntm_physics* p, const ntm_config* c, const double* x, double* rho3) {
+    orc_coef k; orc_coeffs(p, c, &k); orc_rho(&k, x, rho3); return 0;
+}
+
+EXPORT int ntm_oracle_lift(const ntm_physics* p, const ntm_config* c, const double* rho,
+                           double* Phi, double* Gam, double* Lam) {
+    if (!valid(c)) return NTM_E_INVALID;
+    orc_coef k; orc_coeffs(p, c, &k); orc_lift(&k, c, rho, Phi, Gam, Lam); return 0;
+}
+
+EXPORT int ntm_oracle_cost(const ntm_physics* p, const ntm_config* c, const double* rho,
+                           const double* x, double* G, double* F) {
+    if (!valid(c)) return NTM_E_INVALID;
+    orc_coef k; orc_coeffs(p, c, &k);
+    double Phi[2 * NMAX * 2], Gam[2 * NMAX * NMAX], Lam[2 * NMAX];
+    orc_lift(&k, c, rho, Phi, Gam, Lam); orc_cost(c, Phi, Gam, Lam, x, G, F); return 0;
+}
+
+EXPORT int ntm_oracle_getwlc(const ntm_physics* p, const ntm_config* c, const double* rho,
+                             double* W, double* L, double* cv) {
+    if (!valid(c)) return NTM_E_INVALID;
+    orc_coef k; orc_coeffs(p, c, &k);
+    double Phi[2 * NMAX * 2], Gam[2 * NMAX * NMAX], Lam[2 * NMAX];
+    orc_lift(&k, c, rho, Phi, Gam, Lam); orc_getwlc(c, Phi, Gam, Lam, W, L, cv); return 0;
+}
+
+EXPORT int ntm_oracle_qp(int n, int m, const double* G, const double* F, const double* Lin,
+                         const double* b, double* U, int* iters) {
+    if (n < 1 || n > NMAX || m < 0 || m > MMAX) return NTM_E_INVALID;
+    return orc_qp(n, m, G, F, Lin, b, U, iters);
+}
+
+/* Batched MPC step, SoA scenario-minor layout (see include/ntm_mpc.h). */
+EXPORT int ntm_oracle_step(const ntm_physics* p, const ntm_config* c, int64_t B,
+                           const double* x_k, double* rho, double* U_old, double* U,
+                           double* x_pred, double* x_next, int32_t* exitflag,
+                           int32_t* inner_iters, int nthreads) {
+    if (!valid(c) || B < 0) return NTM_E_INVALID;
+    orc_coef k; orc_coeffs(p, c, &k);
+    int N = c->N;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 16)
+#endif
+    for (int64_t s = 0; s < B; ++s) {
+        double x[2], rh[3 * NMAX], uo[NMAX], u[NMAX], xp[2 * (NMAX + 1)], xn[2];
+        int fl, its;
+        for (int e = 0; e < 2; ++e) x[e] = x_k[e * B + s];
+        for (int e = 0; e < 3 * N; ++e) rh[e] = rho[e * B + s];
+        for (int e = 0; e < N; ++e) uo[e] = U_old[e * B + s];
+        orc_step(&k, c, x, rh, uo, u, xp, xn, &fl, &its);
+        for (int e = 0; e < 3 * N; ++e) rho[e * B + s] = rh[e];
+        for (int e = 0; e < N; ++e) { U_old[e * B + s] = uo[e]; U[e * B + s] = u[e]; }
+        for (int e = 0; e < 2 * (N + 1); ++e) x_pred[e * B + s] = xp[e];
+        for (int e = 0; e < 2; ++e) x_next[e * B + s] = xn[e];
+        exitflag[s] = fl;
+        inner_iters[s] = its;
+    }
+    return 0;
+}
+
+/* Batched closed loop NTM_MPC_Sim.m:80-131.  Output layouts as ntm_mpc_run. */
+EXPORT int ntm_oracle_run(const ntm_physics* p, const ntm_config* c, int64_t B, int32_t k_sim,
+                          const double* x0, double* xk, double* uk, double* Uk, double* wpred,
+                          int32_t* exitflag, int32_t* inner_iters, int nthreads) {
+    if (!valid(c) || B < 0 || k_sim < 0) return NTM_E_INVALID;
+    orc_coef k; orc_coeffs(p, c, &k);
+    int N = c->N;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+    for (int64_t s = 0; s < B; ++s) {
+        double x[2], rh[3 * NMAX], uo[NMAX], u[NMAX], xp[2 * (NMAX + 1)], xn[2];
+        x[0] = x0[s]; x[1] = x0[B + s];
+        orc_rho(&k, x, rh);
+        for (int i = 1; i < N; ++i) for (int e = 0; e < 3; ++e) rh[3 * i + e] = rh[e];
+        for (int j = 0; j < N; ++j) uo[j] = INFINITY;
+        if (xk) { xk[s] = x[0]; xk[B + s] = x[1]; }
+        for (int kk = 0; kk < k_sim; ++kk) {
+            int fl, its;
+            orc_step(&k, c, x, rh, uo, u, xp, xn, &fl, &its);
+            if (uk) uk[(int64_t)kk * B + s] = u[0];
+            if (Uk) for (int j = 0; j < N; ++j) Uk[((int64_t)kk * N + j) * B + s] = u[j];
+            if (wpred) for (int i = 0; i <= N; ++i) wpred[((int64_t)kk * (N + 1) + i) * B + s] = xp[2 * i];
+            if (exitflag) exitflag[(int64_t)kk * B + s] = fl;
+            if (inner_iters) inner_iters[(int64_t)kk * B + s] = its;
+            x[0] = xn[0]; x[1] = xn[1];
+            if (xk) { xk[(int64_t)(2 * (kk + 1)) * B + s] = x[0]; xk[(int64_t)(2 * (kk + 1) + 1) * B + s] = x[1]; }
+        }
+    }
+    return 0;
+}
