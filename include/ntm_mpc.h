@@ -84,6 +84,10 @@ typedef struct ntm_ctx ntm_ctx;
 int ntm_ctx_create(ntm_ctx** out, int32_t device);
 void ntm_ctx_destroy(ntm_ctx* ctx);
 const char* ntm_last_error(const ntm_ctx* ctx);
+/* Optional instrumentation: device array of 4*B int32 (SoA) that subsequent
+ * step/run launches ACCUMULATE into: QP solves, Goldfarb-Idnani iterations,
+ * final active rows, general (state) active rows.  NULL disables. */
+int ntm_ctx_set_stats(ntm_ctx* ctx, int32_t* dev_stats);
 
 /* ---- time-step level: the drop-in for NTM_MPC_Sim.m:94-130 ------------ */
 /* One MPC step for B scenarios.  In/out state per scenario:

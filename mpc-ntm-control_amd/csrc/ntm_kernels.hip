@@ -27,21 +27,33 @@ template <int P>
 __device__ __forceinline__ void load_state(const WS& w, int64_t B, int64_t s, const double* rho,
                                            const double* U_old, int l) {
     const int N = w.N;
-    for (int e = l; e < 3 * N; e += P) w.rho[e] = rho[(int64_t)e * B + s];
-    if (l < N) w.Uold[l] = U_old[(int64_t)l * B + s];
+    for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[(int64_t)e * B + s];
+    if (l < N) w.Uold()[l] = U_old[(int64_t)l * B + s];
     NTM_WSYNC();
 }
 
 // one MPC step on LDS-resident state; returns exit flag, sets *iters
 template <int P>
-__device__ int mpc_step_dev(const Prob& pb, const WS& w, double x0, double x1, int l, int* iters) {
+__device__ int mpc_step_dev(const Prob& pb, const WS& w, double x0, double x1, int l, int* iters,
+                            int64_t B = 0, int64_t s = 0) {
     int flag = NTM_EXIT_OPTIMAL, it;
+    int n_qp = 0, n_gi = 0, n_act = 0, n_gen = 0;
     for (it = 1; it <= pb.i_sim; ++it) {
-        int qi;
-        flag = qp_phase<P>(pb, w, x0, x1, l, &qi);
+        int qi = 0, qa = 0, ns = 0;
+        flag = qp_phase<P>(pb, w, x0, x1, l, &qi, &qa, &ns, (it - 1) & 1);
+        ++n_qp;
+        n_gi += qi;
+        n_act += qa;
+        n_gen += ns;
         if (rollout_phase<P>(pb, w, x0, x1, l)) break;
     }
     *iters = it > pb.i_sim ? pb.i_sim : it;
+    if (pb.stats && l == 0) {
+        pb.stats[s] += n_qp;
+        pb.stats[B + s] += n_gi;
+        pb.stats[2 * B + s] += n_act;
+        pb.stats[3 * B + s] += n_gen;
+    }
     return flag;
 }
 
@@ -59,18 +71,19 @@ __global__ __launch_bounds__(64) void k_mpc_step(Prob pb, int64_t B, const doubl
     if (s >= B) return;
     WS w = ws_carve(smem + g * ws_bytes(N), N);
     const double x0 = x_k[s], x1 = x_k[B + s];
+    if (l < 2) w.cand()[l * (N + 1) + N] = -1;
     load_state<P>(w, B, s, rho, U_old, l);
     int its;
-    int flag = mpc_step_dev<P>(pb, w, x0, x1, l, &its);
-    for (int e = l; e < 3 * N; e += P) rho[(int64_t)e * B + s] = w.rho[e];
+    int flag = mpc_step_dev<P>(pb, w, x0, x1, l, &its, B, s);
+    for (int e = l; e < 3 * N; e += P) rho[(int64_t)e * B + s] = w.rho()[e];
     if (l < N) {
-        U_old[(int64_t)l * B + s] = w.Uold[l];
-        U[(int64_t)l * B + s] = w.U[l];
+        U_old[(int64_t)l * B + s] = w.Uold()[l];
+        U[(int64_t)l * B + s] = w.U()[l];
     }
-    for (int e = l; e < 2 * (N + 1); e += P) x_pred[(int64_t)e * B + s] = w.xp[e];
+    for (int e = l; e < 2 * (N + 1); e += P) x_pred[(int64_t)e * B + s] = w.xp()[e];
     if (l == 0) {
         double n0, n1;
-        plant_step(pb, x0, x1, w.U[0], n0, n1);
+        plant_step(pb, x0, x1, w.U()[0], n0, n1);
         x_next[s] = n0;
         x_next[B + s] = n1;
         exitflag[s] = flag;
@@ -90,27 +103,28 @@ __global__ __launch_bounds__(64) void k_mpc_run(Prob pb, int64_t B, int k_sim, c
     if (s >= B) return;
     WS w = ws_carve(smem + g * ws_bytes(N), N);
     double x0 = x0v[s], x1 = x0v[B + s];
+    if (l < 2) w.cand()[l * (N + 1) + N] = -1;
     {   // Rho = repmat(rho(x0), 1, N) (NTM_MPC_Sim.m:63-65); Uold = +inf (D14)
         double r1, r2, r3;
         rho_eval(pb.k, x0, x1, r1, r2, r3);
         if (l < N) {
-            w.rho[3 * l] = r1;
-            w.rho[3 * l + 1] = r2;
-            w.rho[3 * l + 2] = r3;
-            w.Uold[l] = kInf;
+            w.rho()[3 * l] = r1;
+            w.rho()[3 * l + 1] = r2;
+            w.rho()[3 * l + 2] = r3;
+            w.Uold()[l] = kInf;
         }
         NTM_WSYNC();
     }
     if (xk && l == 0) { xk[s] = x0; xk[B + s] = x1; }
     for (int kk = 0; kk < k_sim; ++kk) {
         int its;
-        int flag = mpc_step_dev<P>(pb, w, x0, x1, l, &its);
-        if (Uk && l < N) Uk[((int64_t)kk * N + l) * B + s] = w.U[l];
-        if (wpred) for (int i = l; i <= N; i += P) wpred[((int64_t)kk * (N + 1) + i) * B + s] = w.xp[2 * i];
+        int flag = mpc_step_dev<P>(pb, w, x0, x1, l, &its, B, s);
+        if (Uk && l < N) Uk[((int64_t)kk * N + l) * B + s] = w.U()[l];
+        if (wpred) for (int i = l; i <= N; i += P) wpred[((int64_t)kk * (N + 1) + i) * B + s] = w.xp()[2 * i];
         double n0, n1;
-        plant_step(pb, x0, x1, w.U[0], n0, n1);
+        plant_step(pb, x0, x1, w.U()[0], n0, n1);
         if (l == 0) {
-            if (uk) uk[(int64_t)kk * B + s] = w.U[0];
+            if (uk) uk[(int64_t)kk * B + s] = w.U()[0];
             if (exitflag) exitflag[(int64_t)kk * B + s] = flag;
             if (inner_iters) inner_iters[(int64_t)kk * B + s] = its;
             if (xk) { xk[(int64_t)(2 * kk + 2) * B + s] = n0; xk[(int64_t)(2 * kk + 3) * B + s] = n1; }
@@ -154,19 +168,19 @@ __global__ __launch_bounds__(64) void k_lift(Prob pb, int64_t B, const double* r
     const int N = pb.N, R = 2 * N;
     if (s >= B) return;
     WS w = ws_carve(smem + g * ws_bytes(N), N);
-    for (int e = l; e < 3 * N; e += P) w.rho[e] = rho[(int64_t)e * B + s];
+    for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[(int64_t)e * B + s];
     NTM_WSYNC();
     lift_phase<P>(pb, w, l);
     for (int i = l; i < N; i += P) {
-        const double* Ph = w.Phi + 4 * i;
+        const double* Ph = w.Phi() + 4 * i;
         Phi[(int64_t)(2 * i) * B + s] = Ph[0];
         Phi[(int64_t)(2 * i + 1) * B + s] = Ph[1];
         Phi[(int64_t)(R + 2 * i) * B + s] = Ph[2];
         Phi[(int64_t)(R + 2 * i + 1) * B + s] = Ph[3];
-        Lam[(int64_t)(2 * i) * B + s] = w.Lam[2 * i];
-        Lam[(int64_t)(2 * i + 1) * B + s] = w.Lam[2 * i + 1];
+        Lam[(int64_t)(2 * i) * B + s] = w.Lam()[2 * i];
+        Lam[(int64_t)(2 * i + 1) * B + s] = w.Lam()[2 * i + 1];
     }
-    for (int e = l; e < R * N; e += P) Gam[(int64_t)e * B + s] = w.Gt[e];
+    for (int e = l; e < R * N; e += P) Gam[(int64_t)e * B + s] = w.Gt()[e];
 }
 
 template <int P>
@@ -179,18 +193,18 @@ __global__ __launch_bounds__(64) void k_cost(Prob pb, int64_t B, const double* r
     const int N = pb.N;
     if (s >= B) return;
     WS w = ws_carve(smem + g * ws_bytes(N), N);
-    for (int e = l; e < 3 * N; e += P) w.rho[e] = rho[(int64_t)e * B + s];
+    for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[(int64_t)e * B + s];
     NTM_WSYNC();
     lift_phase<P>(pb, w, l);
     free_response<P>(w, x[s], x[B + s], l);
     cost_phase<P>(pb, w, l);
     if (l < N) {
         for (int kk = 0; kk <= l; ++kk) {
-            double v = w.R[l + kk * w.LDJ];
+            double v = w.R()[l + kk * w.LDJ];
             G_out[(int64_t)(l + kk * N) * B + s] = v;
             G_out[(int64_t)(kk + l * N) * B + s] = v;
         }
-        F_out[(int64_t)l * B + s] = w.F[l];
+        F_out[(int64_t)l * B + s] = w.F()[l];
     }
 }
 
@@ -205,7 +219,7 @@ __global__ __launch_bounds__(64) void k_getwlc(Prob pb, int64_t B, const double*
     const int N = pb.N, m = 6 * N + 4;
     if (s >= B) return;
     WS w = ws_carve(smem + g * ws_bytes(N), N);
-    for (int e = l; e < 3 * N; e += P) w.rho[e] = rho[(int64_t)e * B + s];
+    for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[(int64_t)e * B + s];
     NTM_WSYNC();
     lift_phase<P>(pb, w, l);
     for (int row = l; row < m; row += P) {
@@ -227,10 +241,10 @@ __global__ __launch_bounds__(64) void k_getwlc(Prob pb, int64_t B, const double*
                 if (cc == 0) Wr0 = -sg; else Wr1 = -sg;
             } else {
                 int r = 2 * (i - 1) + cc;
-                for (int j = 0; j < N; ++j) L[((int64_t)row + (int64_t)j * m) * B + s] = sg * w.Gt[r + j * w.LDG];
-                Wr0 = -sg * w.Phi[4 * (i - 1) + cc];
-                Wr1 = -sg * w.Phi[4 * (i - 1) + 2 + cc];
-                cr -= sg * w.Lam[r];
+                for (int j = 0; j < N; ++j) L[((int64_t)row + (int64_t)j * m) * B + s] = sg * w.Gt()[r + j * w.LDG];
+                Wr0 = -sg * w.Phi()[4 * (i - 1) + cc];
+                Wr1 = -sg * w.Phi()[4 * (i - 1) + 2 + cc];
+                cr -= sg * w.Lam()[r];
             }
         }
         W[(int64_t)row * B + s] = Wr0;
@@ -254,25 +268,33 @@ __global__ __launch_bounds__(64) void k_qp(int64_t B, int N, int m, const double
     WS w = ws_carve(base, N);
     double* rnrm = reinterpret_cast<double*>(base + ws_bytes(N));
     if (l < N) {
-        for (int kk = 0; kk <= l; ++kk) w.R[l + kk * w.LDJ] = G_in[((int64_t)l + (int64_t)kk * N) * B + s];
-        w.F[l] = F_in[(int64_t)l * B + s];
+        for (int kk = 0; kk <= l; ++kk) w.R()[l + kk * w.LDJ] = G_in[((int64_t)l + (int64_t)kk * N) * B + s];
+        w.F()[l] = F_in[(int64_t)l * B + s];
     }
-    for (int i = l; i < m; i += P) w.aflag[i] = 0;
+    for (int i = l; i < m; i += P) w.aflag()[i] = 0;
     NTM_WSYNC();
-    int flag, its = 0;
+    int flag, its = 0, q = 0;
+    DenseRows rows{Lin, b, rnrm, B, s, m};
     if (!scale_phase<P>(w, l, false)) {
         flag = NTM_EXIT_NONFINITE;
     } else {
-        DenseRows rows{Lin, b, rnrm, B, s, m};
         int code = rows.template prepare_code<P>(w, l);
         if (code & 1) flag = NTM_EXIT_NONFINITE;
         else if (code & 2) flag = NTM_EXIT_INFEASIBLE;
-        else flag = gi_solve<P, DenseRows>(w, m > 0 ? &rows : nullptr, m, l, &its);
+        else {
+            // keep G~ for the polish (w.Gt() is unused without a lifted model)
+            if (l < N) for (int j = 0; j <= l; ++j) w.Gt()[l + j * w.LDJ] = w.R()[l + j * w.LDJ];
+            NTM_WSYNC();
+            flag = gi_solve<P, DenseRows>(w, m > 0 ? &rows : nullptr, m, l, &its, &q);
+        }
     }
-    if (l < N) {
-        double u = (flag == NTM_EXIT_OPTIMAL || flag == NTM_EXIT_MAXITER) ? w.V[l] * w.D[l] : 0.0;
-        U[(int64_t)l * B + s] = u;
+    if (flag == NTM_EXIT_OPTIMAL) {
+        (void)polish_phase<P, DenseRows>(Prob{}, w, &rows, q, l, w.Gt(), false, false, nullptr);
+    } else if (l < N) {
+        w.U()[l] = (flag == NTM_EXIT_MAXITER) ? w.V()[l] * w.D()[l] : 0.0;
     }
+    NTM_WSYNC();
+    if (l < N) U[(int64_t)l * B + s] = w.U()[l];
     if (l == 0) {
         exitflag[s] = flag;
         if (iters) iters[s] = its;
@@ -323,6 +345,7 @@ int lanes_for(int N) { return N <= 16 ? 16 : (N <= 32 ? 32 : 64); }
 // =========================================================================
 struct ntm_ctx {
     int device = 0;
+    int32_t* stats = nullptr;   // optional device counters (ntm_ctx_set_stats)
     std::string err;
     void* dbuf = nullptr;
     size_t dbuf_bytes = 0;
@@ -488,6 +511,12 @@ void ntm_ctx_destroy(ntm_ctx* ctx) {
 
 const char* ntm_last_error(const ntm_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+int ntm_ctx_set_stats(ntm_ctx* ctx, int32_t* dev_stats) {
+    if (!ctx) return NTM_E_INVALID;
+    ctx->stats = dev_stats;
+    return NTM_OK;
+}
+
 int ntm_mpc_step_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B,
                         const double* x_k, double* rho, double* U_old, double* U, double* x_pred, double* x_next,
                         int32_t* exitflag, int32_t* inner_iters, void* stream) {
@@ -497,6 +526,7 @@ int ntm_mpc_step_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config*
     if (!x_k || !rho || !U_old || !U || !x_pred || !x_next || !exitflag || !inner_iters)
         return fail(ctx, NTM_E_INVALID, "null array");
     Prob pb = make_prob(phys, cfg);
+    pb.stats = ctx->stats;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define CALL(P) launch_step<P>(ctx, pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, st)
     return NTM_DISPATCH_P(cfg->N, CALL);
@@ -551,6 +581,7 @@ int ntm_mpc_run_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* 
     if (B == 0) return NTM_OK;
     if (!x0) return fail(ctx, NTM_E_INVALID, "null x0");
     Prob pb = make_prob(phys, cfg);
+    pb.stats = ctx->stats;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define CALL(P) launch_run<P>(ctx, pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, st)
     return NTM_DISPATCH_P(cfg->N, CALL);

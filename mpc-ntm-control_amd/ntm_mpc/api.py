@@ -142,6 +142,14 @@ class NtmMpc:
     def _empty(self, *shape, dtype=torch.float64):
         return torch.empty(*shape, dtype=dtype, device=f"cuda:{self.device}")
 
+    def set_stats(self, stats: torch.Tensor | None):
+        """Accumulate per-scenario counters (4, B) int32 into ``stats`` during
+        subsequent step/run launches (QP solves, GI iterations, final active
+        rows, state rows in the final active set); None disables."""
+        if stats is not None:
+            _check_dev(stats, tuple(stats.shape), dtype=torch.int32, name="stats")
+        self._raise(self.lib.ntm_ctx_set_stats(self._ctx, _ptr(stats)), "ntm_ctx_set_stats")
+
     # ------------------------------------------------------------ hot path
     def initial_state(self, x0: torch.Tensor, cfg: Config | None = None):
         """Rho = repmat(rho(x0), 1, N) (NTM_MPC_Sim.m:63-65); U_old = +inf (D14)."""

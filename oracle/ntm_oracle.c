@@ -193,6 +193,11 @@ static void orc_getwlc(const ntm_config* c, const double* Phi, const double* Gam
     }
 }
 
+static double gi_dep_tol = 1e-8;
+static int gi_polish = 1;
+__attribute__((visibility("default"))) void ntm_oracle_set_polish(int on) { gi_polish = on; }
+__attribute__((visibility("default"))) void ntm_oracle_set_dep_tol(double t) { gi_dep_tol = t; }
+
 /* ------------------------------------------------------------------ */
 /* Goldfarb-Idnani dual active set: min 1/2 U'GU + F'U  s.t. Lin U <= b. */
 /* ------------------------------------------------------------------ */
@@ -203,7 +208,7 @@ static void givens(double a, double b, double* cc, double* ss, double* h) {
 }
 
 static int orc_gi(int n, int m, const double* G, const double* F, const double* Lin,
-                  const double* b, double* U, int* iters_out) {
+                  const double* b, double* U, int* iters_out, int* act_out, int* q_out) {
     double J[NMAX * NMAX], Rm[NMAX * NMAX], Lc[NMAX * NMAX];
     double up[NMAX + 1], d[NMAX], z[NMAX], r[NMAX];
     static const int max_extra = 50;
@@ -272,9 +277,11 @@ static int orc_gi(int n, int m, const double* G, const double* F, const double* 
             double v = s / nrm[i];
             if (p < 0 || v < best) { best = v; p = i; sp_best = s; }
         }
-        if (p < 0) { *iters_out = it; return NTM_EXIT_OPTIMAL; }
-        double tolp = 1e-12 * fmax(nrm[p] * umax_abs, fabs(b[p]));
-        if (sp_best >= -tolp) { *iters_out = it; return NTM_EXIT_OPTIMAL; }
+        if (p < 0 || sp_best >= -1e-12 * fmax(nrm[p] * umax_abs, fabs(b[p]))) {
+            *iters_out = it;
+            if (act_out) { for (int a = 0; a < q; ++a) act_out[a] = act[a]; *q_out = q; }
+            return NTM_EXIT_OPTIMAL;
+        }
         double np_[NMAX];
         for (int j = 0; j < n; ++j) np_[j] = -Lin[(size_t)j * m + p];
         up[q] = 0.0;
@@ -296,17 +303,22 @@ static int orc_gi(int n, int m, const double* G, const double* F, const double* 
             double t1 = INFINITY; int l = -1;
             for (int a = 0; a < q; ++a)
                 if (r[a] > 0.0) { double ta = up[a] / r[a]; if (ta < t1) { t1 = ta; l = a; } }
+            /* z'n_p = |d2|^2 exactly (z = J2 d2): computed that way it can never
+             * be negative; n_p is treated as dependent on the active rows when
+             * |d2| <= GI_DEP_TOL |d| (consecutive w-rows plus a u-bound are
+             * dependent up to a11 - 1 ~ 5e-10). */
             double zn = 0.0, sp = b[p];                   /* sp = n_p'U - bc_p */
-            for (int j = 0; j < n; ++j) { zn += z[j] * np_[j]; sp += np_[j] * U[j]; }
-            double t2 = (fabs(zn) <= 1e-300 || sqrt(znrm) <= 1e-14 * sqrt(dnrm)) ? INFINITY : -sp / zn;
+            for (int kk = q; kk < n; ++kk) zn += d[kk] * d[kk];
+            for (int j = 0; j < n; ++j) sp += np_[j] * U[j];
+            double t2 = (zn <= 1e-300 || sqrt(zn) <= gi_dep_tol * sqrt(dnrm)) ? INFINITY : -sp / zn;
             double t = t1 < t2 ? t1 : t2;
             if (t == INFINITY) { for (int j = 0; j < n; ++j) U[j] = 0.0; *iters_out = it; return NTM_EXIT_INFEASIBLE; }
             if (t2 == INFINITY) {
-                for (int a = 0; a < q; ++a) up[a] -= t * r[a];
+                for (int a = 0; a < q; ++a) up[a] = fmax(0.0, up[a] - t * r[a]);
                 up[q] += t;
             } else {
                 for (int j = 0; j < n; ++j) U[j] += t * z[j];
-                for (int a = 0; a < q; ++a) up[a] -= t * r[a];
+                for (int a = 0; a < q; ++a) up[a] = fmax(0.0, up[a] - t * r[a]);
                 up[q] += t;
                 if (t == t2) {                                 /* add constraint p */
                     for (int kk = n - 1; kk > q; --kk) {
@@ -350,6 +362,139 @@ static int orc_gi(int n, int m, const double* G, const double* F, const double* 
     }
 }
 
+/* left-looking Cholesky of the n x n (row-major) A into L (row-major lower); 0 if not PD */
+static int chol_rm(int n, const double* A, double* L) {
+    for (int k = 0; k < n; ++k) {
+        for (int i = k; i < n; ++i) {
+            double s = A[i * n + k];
+            for (int j = 0; j < k; ++j) s -= L[i * n + j] * L[k * n + j];
+            if (i == k) {
+                if (!(s > 0.0)) return 0;
+                L[k * n + k] = sqrt(s);
+            } else {
+                L[i * n + k] = s / L[k * n + k];
+            }
+        }
+        for (int j = k + 1; j < n; ++j) L[k * n + j] = 0.0;
+    }
+    return 1;
+}
+static void fwd_rm(int n, const double* L, const double* b, double* x) {
+    for (int i = 0; i < n; ++i) {
+        double s = b[i];
+        for (int k = 0; k < i; ++k) s -= L[i * n + k] * x[k];
+        x[i] = s / L[i * n + i];
+    }
+}
+static void bwd_rm(int n, const double* L, const double* b, double* x) {   /* L' x = b */
+    for (int i = n - 1; i >= 0; --i) {
+        double s = b[i];
+        for (int k = i + 1; k < n; ++k) s -= L[k * n + i] * x[k];
+        x[i] = s / L[i * n + i];
+    }
+}
+
+/* Exact re-solve on GI's final active set (see oracle/ntm_oracle.py
+ * polish_active_set).  Gs/Ls/bs: scaled, normalised data
+ * (Lin U <= b form); Lin/b: unscaled.  Writes U and returns 1 when the KKT
+ * certificate holds. */
+static int orc_polish(int n, int m, const double* Gs, const double* Fs, const double* Ls,
+                      const double* bs, const double* Lin, const double* b, const double* D,
+                      const int* act, int q, double* U) {
+    static __thread double Gm[NMAX * NMAX], Lc[NMAX * NMAX], Y[NMAX * NMAX], K[NMAX * NMAX], Lk[NMAX * NMAX];
+    double Vb[NMAX], Ufix[NMAX], g[NMAX], w[NMAX], V[NMAX], mu[NMAX], tmp[NMAX], h[NMAX];
+    unsigned char fixed[NMAX];
+    int S[NMAX], nS = 0;
+    memset(fixed, 0, sizeof fixed);
+    for (int j = 0; j < n; ++j) Vb[j] = 0.0;
+    for (int a = 0; a < q; ++a) {
+        int row = act[a], nzc = 0, jj = -1;
+        for (int j = 0; j < n; ++j) if (Lin[(size_t)j * m + row] != 0.0) { ++nzc; jj = j; }
+        if (nzc == 1) {
+            Ufix[jj] = b[row] / Lin[(size_t)jj * m + row];
+            Vb[jj] = Ufix[jj] / D[jj];
+            fixed[jj] = 1;
+        } else {
+            S[nS++] = row;
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        double s = Fs[i];
+        for (int j = 0; j < n; ++j) if (fixed[j]) s += Gs[(size_t)j * n + i] * Vb[j];
+        g[i] = fixed[i] ? 0.0 : s;
+        for (int j = 0; j < n; ++j)
+            Gm[i * n + j] = (fixed[i] || fixed[j]) ? (i == j ? 1.0 : 0.0) : Gs[(size_t)j * n + i];
+    }
+    if (!chol_rm(n, Gm, Lc)) return 0;
+    fwd_rm(n, Lc, g, w);
+    if (nS > 0) {
+        for (int k = 0; k < nS; ++k) {
+            double e[NMAX], y[NMAX], hk = -bs[S[k]];           /* bc = -bs, n = -Ls */
+            for (int j = 0; j < n; ++j) {
+                double nj = -Ls[(size_t)j * m + S[k]];
+                if (fixed[j]) { hk -= nj * Vb[j]; e[j] = 0.0; } else e[j] = nj;
+            }
+            h[k] = hk;
+            fwd_rm(n, Lc, e, y);
+            for (int i = 0; i < n; ++i) Y[i * NMAX + k] = y[i];
+        }
+        for (int a = 0; a < nS; ++a)
+            for (int c2 = 0; c2 < nS; ++c2) {
+                double s = 0.0;
+                for (int i = 0; i < n; ++i) s += Y[i * NMAX + a] * Y[i * NMAX + c2];
+                K[a * nS + c2] = s;
+            }
+        if (!chol_rm(nS, K, Lk)) return 0;
+        for (int a = 0; a < nS; ++a) {
+            double s = h[a];
+            for (int i = 0; i < n; ++i) s += Y[i * NMAX + a] * w[i];
+            tmp[a] = s;
+        }
+        double t2[NMAX];
+        fwd_rm(nS, Lk, tmp, t2);
+        bwd_rm(nS, Lk, t2, mu);
+        for (int i = 0; i < n; ++i) {
+            double s = -w[i];
+            for (int a = 0; a < nS; ++a) s += Y[i * NMAX + a] * mu[a];
+            tmp[i] = s;
+        }
+        bwd_rm(n, Lc, tmp, V);
+    } else {
+        for (int i = 0; i < n; ++i) tmp[i] = -w[i];
+        bwd_rm(n, Lc, tmp, V);
+    }
+    for (int j = 0; j < n; ++j) if (fixed[j]) V[j] = Vb[j];
+    /* KKT certificate: primal slack on every non-constant row, multiplier signs */
+    double vmax = 1.0;
+    for (int j = 0; j < n; ++j) if (fabs(V[j]) > vmax) vmax = fabs(V[j]);
+    for (int i = 0; i < m; ++i) {
+        double s = bs[i], nz2 = 0.0;
+        for (int j = 0; j < n; ++j) { double l = Ls[(size_t)j * m + i]; s -= l * V[j]; nz2 += l * l; }
+        if (nz2 > 0.0 && s < -1e-9 * fmax(vmax, fabs(bs[i]))) return 0;
+    }
+    double res[NMAX], mults[2 * NMAX], mscale = 1.0;
+    int nm = 0;
+    for (int i = 0; i < n; ++i) {
+        double s = Fs[i];
+        for (int j = 0; j < n; ++j) s += Gs[(size_t)j * n + i] * V[j];
+        for (int k = 0; k < nS; ++k) s -= mu[k] * (-Ls[(size_t)i * m + S[k]]);
+        res[i] = s;
+    }
+    for (int k = 0; k < nS; ++k) mults[nm++] = mu[k];
+    for (int a = 0; a < q; ++a) {
+        int row = act[a], isS = 0;
+        for (int k = 0; k < nS; ++k) if (S[k] == row) isS = 1;
+        if (isS) continue;
+        for (int j = 0; j < n; ++j)
+            if (Lin[(size_t)j * m + row] != 0.0) { mults[nm++] = res[j] / (-Ls[(size_t)j * m + row]); break; }
+    }
+    double mmin = 0.0;
+    for (int k = 0; k < nm; ++k) { if (fabs(mults[k]) > mscale) mscale = fabs(mults[k]); if (mults[k] < mmin) mmin = mults[k]; }
+    if (mmin < -1e-9 * mscale) return 0;
+    for (int j = 0; j < n; ++j) U[j] = fixed[j] ? Ufix[j] : V[j] * D[j];
+    return 1;
+}
+
 /* quadprog stand-in: Jacobi variable scaling U = D V (diag(DGD) = 1) and
  * unit-norm constraint rows, then Goldfarb-Idnani on the scaled problem
  * (cond(G) ~1e9-1e11 drops to ~1e6; see oracle/ntm_oracle.py qp_solve). */
@@ -372,8 +517,10 @@ static int orc_qp(int n, int m, const double* G, const double* F, const double* 
         for (int j = 0; j < n; ++j) Ls[(size_t)j * m + i] /= rn;
         bs[i] = b[i] / rn;
     }
-    int flag = orc_gi(n, m, Gs, Fs, Ls, bs, V, iters_out);
+    int act[NMAX + 1], q = 0;
+    int flag = orc_gi(n, m, Gs, Fs, Ls, bs, V, iters_out, act, &q);
     for (int j = 0; j < n; ++j) U[j] = V[j] * D[j];
+    if (flag == NTM_EXIT_OPTIMAL && gi_polish) (void)orc_polish(n, m, Gs, Fs, Ls, bs, Lin, b, D, act, q, U);
     return flag;
 }
 

@@ -284,6 +284,7 @@ def constraints(Phi, Gamma, Lam, xk, cfg: Config):
 # --------------------------------------------------------------------------
 
 EXIT_OK, EXIT_MAXIT, EXIT_INFEASIBLE, EXIT_NONFINITE = 1, 0, -2, -7
+GI_DEP_TOL = 1e-8
 
 
 def _givens(a, b):
@@ -350,21 +351,23 @@ def qp_dual_active_set(G, F, Lin, b, max_iter=None):
                     tj = up[j] / r[j]
                     if tj < t1:
                         t1, l = tj, j
-            zn = float(z @ Nc[p])
+            # z'n_p = |d2|^2 (z = J2 d2): never negative; n_p counts as dependent
+            # on the active rows when |d2| <= GI_DEP_TOL |d|
+            zn = float(d[q:] @ d[q:])
             sp = float(Nc[p] @ U - bc[p])
-            t2 = math.inf if abs(zn) <= 1e-300 or np.linalg.norm(z) <= 1e-14 * np.linalg.norm(d) else -sp / zn
+            t2 = math.inf if zn <= 1e-300 or math.sqrt(zn) <= GI_DEP_TOL * np.linalg.norm(d) else -sp / zn
             t = min(t1, t2)
             if t == math.inf:
                 return np.zeros(n), EXIT_INFEASIBLE, act, up[:q], it
             if t2 == math.inf:
-                up[:q] -= t * r
+                up[:q] = np.maximum(0.0, up[:q] - t * r)
                 up[q] += t
                 J, R = _drop(J, R, q, l)
                 act.pop(l)
                 up = np.delete(up, l)
                 continue
             U = U + t * z
-            up[:q] -= t * r
+            up[:q] = np.maximum(0.0, up[:q] - t * r)
             up[q] += t
             if t == t2:
                 J, R = _add(J, R, q, d)
@@ -444,6 +447,112 @@ def kkt_polish(G, F, Lin, b, act, dps=50):
                                                       "min_multiplier": float(lam_min)}
 
 
+def _chol_lower(A):
+    """Left-looking Cholesky (the order the GPU and the C oracle use); None if not PD."""
+    n = A.shape[0]
+    L = np.zeros_like(A)
+    for k in range(n):
+        s = A[k:, k] - L[k:, :k] @ L[k, :k]
+        if not s[0] > 0.0:
+            return None
+        lk = math.sqrt(s[0])
+        L[k, k] = lk
+        L[k + 1:, k] = s[1:] / lk
+    return L
+
+
+def _fwd(L, b):
+    x = np.zeros_like(b, dtype=float)
+    for i in range(L.shape[0]):
+        x[i] = (b[i] - L[i, :i] @ x[:i]) / L[i, i]
+    return x
+
+
+def _bwd(L, b):
+    """Solve L' x = b (L lower)."""
+    n = L.shape[0]
+    x = np.zeros_like(b, dtype=float)
+    for i in range(n - 1, -1, -1):
+        x[i] = (b[i] - L[i + 1:, i] @ x[i + 1:]) / L[i, i]
+    return x
+
+
+POLISH_PRIMAL_TOL = 1e-9
+POLISH_DUAL_TOL = 1e-9
+
+
+def polish_active_set(Gs, Fs, Ns, bcs, act, Lin, b, Dv):
+    """Exact re-solve of the scaled QP on GI's final active set.
+
+    Rows with a single non-zero (u bounds, and the w-rows of x_1 which only
+    see u_0) fix their variable: U_j = b_a / Lin_aj exactly.  The remaining
+    active rows S are equality constraints on the free variables F:
+        min 1/2 V_F' G~_FF V_F + g_F' V_F  s.t.  E V_F = h
+    solved with a fresh Cholesky of G~_FF (B rows/cols masked to identity)
+    and of the Schur complement K = E G~_FF^{-1} E'.  The result is accepted
+    only if it passes the KKT check (primal slack, multiplier signs); returns
+    (V, U, ok)."""
+    n = Gs.shape[0]
+    fixed = np.zeros(n, dtype=bool)
+    Vb = np.zeros(n)
+    Ufix = np.zeros(n)
+    S = []
+    for a in act:
+        nz = np.flatnonzero(Lin[a])
+        if len(nz) == 1:
+            j = nz[0]
+            Ufix[j] = b[a] / Lin[a, j]
+            Vb[j] = Ufix[j] / Dv[j]
+            fixed[j] = True
+        else:
+            S.append(a)
+    g = Fs + Gs[:, fixed] @ Vb[fixed]
+    Gm = Gs.copy()
+    Gm[fixed, :] = 0.0
+    Gm[:, fixed] = 0.0
+    Gm[fixed, fixed] = 1.0
+    gm = np.where(fixed, 0.0, g)
+    Lc = _chol_lower(Gm)
+    if Lc is None:
+        return None, None, False
+    w = _fwd(Lc, gm)
+    mu = np.zeros(0)
+    if S:
+        E = Ns[S].copy()
+        h = bcs[S] - E[:, fixed] @ Vb[fixed]
+        E[:, fixed] = 0.0
+        Y = np.stack([_fwd(Lc, E[k]) for k in range(len(S))], axis=1)     # n x nS
+        K = Y.T @ Y
+        Lk = _chol_lower(K)
+        if Lk is None:
+            return None, None, False
+        mu = _bwd(Lk, _fwd(Lk, h + Y.T @ w))
+        V = _bwd(Lc, Y @ mu - w)
+    else:
+        V = _bwd(Lc, -w)
+    V = np.where(fixed, Vb, V)
+    U = np.where(fixed, Ufix, V * Dv)
+    # KKT certificate
+    nzr = np.any(Ns != 0.0, axis=1)
+    slack = Ns @ V - bcs
+    vmax = max(1.0, float(np.max(np.abs(V))))
+    if np.any(nzr & (slack < -POLISH_PRIMAL_TOL * np.maximum(vmax, np.abs(bcs)))):
+        return V, U, False
+    grad = Gs @ V + Fs
+    res = grad - (Ns[S].T @ mu if S else 0.0)
+    lam = []
+    for a in act:
+        if a in S:
+            continue
+        j = np.flatnonzero(Lin[a])[0]
+        lam.append(res[j] / Ns[a, j])
+    mults = np.concatenate([mu, np.asarray(lam)])
+    scale = max(1.0, float(np.max(np.abs(mults))) if len(mults) else 1.0)
+    if len(mults) and np.min(mults) < -POLISH_DUAL_TOL * scale:
+        return V, U, False
+    return V, U, True
+
+
 def jacobi_scale(G):
     """D = diag(1/sqrt(G_jj)) (1 where G_jj <= 0)."""
     dg = np.diag(G)
@@ -474,10 +583,16 @@ def qp_solve(G, F, Lin, b, polish=False):
     Ls = Lin * Dv[None, :]
     rn = np.linalg.norm(Ls, axis=1)
     rn = np.where(rn > 0.0, rn, 1.0)
-    V, flag, act, lam, its = qp_dual_active_set(Gs, F * Dv, Ls / rn[:, None], b / rn)
+    Ns, bcs, Fs = -(Ls / rn[:, None]), -(b / rn), F * Dv
+    V, flag, act, lam, its = qp_dual_active_set(Gs, Fs, -Ns, -bcs)
     U = V * Dv
+    polished = False
+    if flag == EXIT_OK:
+        Vp, Up, ok = polish_active_set(Gs, Fs, Ns, bcs, act, Lin, b, Dv)
+        if ok:
+            U, polished = Up, True
     lam = np.asarray(lam) / rn[act] if len(act) else np.asarray(lam)
-    info = {"active": list(act), "iters": its, "multipliers": lam}
+    info = {"active": list(act), "iters": its, "multipliers": lam, "polished": polished}
     if flag == EXIT_OK and polish:
         U, lam, cert = kkt_polish(G, F, Lin, b, act)
         info["multipliers"] = lam
