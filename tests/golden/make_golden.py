@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures under tests/golden/ from the Python
+oracle (oracle/ntm_oracle.py).  The reference (MATLAB) cannot run in this
+image (no MATLAB/Octave) and ships no fixtures of its own, so these vectors
+are produced by the oracle, whose correctness is pinned by the invariant
+tests in tests/test_oracle.py and by 50-digit KKT certificates stored with
+every QP fixture.  Re-run after any change to the canonical semantics:
+
+    python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import sys
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE.parent.parent))
+from oracle import ntm_oracle as O  # noqa: E402
+
+
+def functions_fixture(N):
+    ph = O.Physics()
+    cfg = O.Config(N=N, mode=O.MODE_FULL)
+    rng = np.random.default_rng(1000 + N)
+    xs = np.stack([rng.uniform(0.06, 0.15, N), rng.uniform(0.8, 1.2, N) * 2000 * np.pi])
+    Rho = np.stack([O.rho_all(xs[:, i], ph, cfg) for i in range(N)], axis=1)       # 3 x N
+    xk = np.array([0.1, 2000 * np.pi])
+    Phi, Gam, Lam = O.lift(Rho, ph, cfg)
+    G, F = O.cost(Phi, Gam, Lam, xk, cfg)
+    W, L, c = O.getWLc(cfg.xmax, cfg.xmin, cfg.umax, cfg.umin, Gam, Phi, Lam)
+    A0 = O.A_mat(Rho[0, 0], Rho[1, 0], ph, cfg.Ts)
+    B0 = O.B_mat(Rho[2, 0], ph, cfg.Ts)
+    np.savez(HERE / f"functions_N{N}.npz", xs=xs, Rho=Rho, xk=xk, Phi=Phi, Gamma=Gam, Lambda=Lam, G=G, F=F,
+             W=W, L=L, c=c, A0=A0, B0=B0, C=O.C_vec(ph, cfg.Ts), kappa=ph.kappa(), zeta=ph.zeta())
+
+
+def closed_loop_fixture(N, mode, ids, k_sim):
+    ph = O.Physics()
+    cfg = O.Config(N=N, mode=mode)
+    x0 = O.scenario_x0(ids) if mode != O.MODE_NONE else np.tile(O.REFERENCE_X0, (len(ids), 1))
+    outs = [O.closed_loop(x0[s], ph, cfg, k_sim) for s in range(len(ids))]
+    np.savez(HERE / f"closed_loop_m{mode}_N{N}.npz", x0=x0, ids=np.asarray(ids),
+             xk=np.stack([o["xk"] for o in outs]), uk=np.stack([o["uk"] for o in outs]),
+             Uk=np.stack([o["Uk"] for o in outs]), exitflag=np.stack([o["exitflag"] for o in outs]),
+             inner_iters=np.stack([o["inner_iters"] for o in outs]), k_sim=k_sim)
+
+
+def qp_fixture(N, mode, n):
+    """QPs met along closed-loop trajectories, with the certified exact optimum."""
+    ph = O.Physics()
+    cfg = O.Config(N=N, mode=mode)
+    Gs, Fs, Ls, bs, Us, flags = [], [], [], [], [], []
+    x0 = O.scenario_x0(np.arange(n))
+    for s in range(n):
+        xk = x0[s]
+        Rho = O.initial_rho(xk, ph, cfg)
+        for it in range(1 + s % 4):
+            Phi, Gam, Lam = O.lift(Rho, ph, cfg)
+            G, F = O.cost(Phi, Gam, Lam, xk, cfg)
+            Lin, b = O.constraints(Phi, Gam, Lam, xk, cfg)
+            U, flag, info = O.qp_solve(G, F, Lin, b)
+            _, Rho = O.rollout(xk, Rho, U, ph, cfg)
+        Phi, Gam, Lam = O.lift(Rho, ph, cfg)
+        G, F = O.cost(Phi, Gam, Lam, xk, cfg)
+        Lin, b = O.constraints(Phi, Gam, Lam, xk, cfg)
+        U, flag, info = O.qp_solve(G, F, Lin, b)
+        Ue, _, cert = O.kkt_polish(G, F, Lin, b, info["active"], dps=50)
+        assert cert["max_violation"] <= 1e-12 and cert["min_multiplier"] >= -1e-12, cert
+        Gs.append(G), Fs.append(F), Ls.append(Lin), bs.append(b), Us.append(Ue), flags.append(flag)
+    np.savez(HERE / f"qp_m{mode}_N{N}.npz", G=np.stack(Gs), F=np.stack(Fs), Lin=np.stack(Ls), b=np.stack(bs),
+             U_exact=np.stack(Us), exitflag=np.asarray(flags))
+
+
+def main():
+    for N in (3, 20):
+        functions_fixture(N)
+    closed_loop_fixture(10, O.MODE_NONE, [0], 20)          # BASELINE config 1
+    closed_loop_fixture(3, O.MODE_FULL, [0, 1, 2, 3], 20)
+    closed_loop_fixture(20, O.MODE_BOX, [0, 1], 6)          # config 2 shape
+    closed_loop_fixture(20, O.MODE_FULL, [0, 1, 2], 6)      # config 3 shape
+    qp_fixture(20, O.MODE_FULL, 12)
+    qp_fixture(20, O.MODE_BOX, 8)
+    print("fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,112 @@
+"""Host-side checks that need no GPU: the HIP library builds for gfx950, loads,
+exports every symbol include/ntm_mpc.h declares, and the Python mirror's
+host logic (configs, defaults, layouts, scenario generator, flop model)."""
+import ctypes as C
+import math
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "ntm_mpc.h"
+
+
+def declared_functions():
+    txt = HEADER.read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(ntm_[A-Za-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    import ntm_mpc
+    lib = ntm_mpc.load()
+    names = declared_functions()
+    assert len(names) >= 17
+    for n in names:
+        assert hasattr(lib, n), n
+    from ntm_mpc._lib import EXPORTS
+    assert set(EXPORTS) == set(names)
+
+
+def test_library_is_gfx950_code_object():
+    import subprocess
+    lib = ROOT / "mpc-ntm-control_amd" / "lib" / "libntm_mpc.so"
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)], capture_output=True,
+                         text=True)
+    assert "gfx950" in (out.stdout + out.stderr)
+
+
+def test_defaults_match_reference_literals():
+    from ntm_mpc import _lib as L
+    from ntm_mpc.api import Config, Physics
+    p = L.default_physics()
+    ref = Physics()
+    for n in L.PHYSICS_FIELDS:
+        assert getattr(p, n) == pytest.approx(getattr(ref, n), rel=1e-15), n
+    c = L.default_config(20)
+    assert (c.N, c.i_sim, c.mode) == (20, 10, 2)
+    assert c.Ts == 0.1 and c.umax == 2e6 and c.umin == 0
+    assert tuple(c.xmin) == pytest.approx((0.06, 200 * math.pi))
+    assert tuple(c.xmax) == pytest.approx((0.15, 10000 * math.pi))
+    assert c.r[1] == pytest.approx(2000 * math.pi) and c.epsilon == 1e-14
+    py = Config(N=20).to_c()
+    for f, _ in L.NtmConfig._fields_:
+        a, b = getattr(py, f), getattr(c, f)
+        if hasattr(a, "__len__"):
+            assert list(a) == pytest.approx(list(b))
+        else:
+            assert a == pytest.approx(b)
+
+
+def test_config_rows():
+    from ntm_mpc.api import Config
+    assert Config(N=20, mode=2).m == 124
+    assert Config(N=20, mode=1).m == 40
+    assert Config(N=20, mode=0).m == 0
+
+
+def test_scenario_generator_matches_oracle():
+    """ntm_scenarios_x0 (C-ABI) == oracle scenario_x0: shard-invariant synthetic inputs."""
+    import ntm_mpc
+    from oracle import ntm_oracle as O
+    x = ntm_mpc.scenarios_x0(1000, 257)
+    np.testing.assert_array_equal(x.T, O.scenario_x0(np.arange(1000, 1257)))
+    a = ntm_mpc.scenarios_x0(0, 10)
+    b = ntm_mpc.scenarios_x0(5, 5)
+    np.testing.assert_array_equal(a[:, 5:], b)
+
+
+def test_no_gpu_raises_not_falls_back():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from ntm_mpc import NtmLibraryError, NtmMpc
+    with pytest.raises(NtmLibraryError):
+        NtmMpc()
+
+
+def test_ctx_create_without_gpu_is_an_error():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import ntm_mpc
+    ctx = C.c_void_p()
+    assert ntm_mpc.load().ntm_ctx_create(C.byref(ctx), 0) != 0
+
+
+def test_flop_model_monotone():
+    from ntm_mpc import flops
+    a = flops.per_step(20, 2, 8, 10, 19, 5)
+    b = flops.per_step(20, 2, 8, 40, 19, 5)
+    assert 0 < a < b
+    assert flops.hbm_bytes_per_step(20) == 8 * (2 + 120 + 40 + 20 + 42 + 2) + 8
+
+
+def test_product_never_imports_oracle():
+    """The product package must not import, link or execute the oracle (checker)."""
+    pkg = ROOT / "mpc-ntm-control_amd"
+    bad = re.compile(r"(import\s+oracle|from\s+oracle|libntm_oracle|cbind|ntm_oracle_)")
+    for f in list(pkg.rglob("*.py")) + list(pkg.rglob("*.hip")) + list(pkg.rglob("*.h")) + [pkg / "Makefile"]:
+        assert not bad.search(f.read_text()), f

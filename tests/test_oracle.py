@@ -1,0 +1,278 @@
+"""Pin the CPU oracle (oracle/ntm_oracle.py) to the reference.
+
+The MATLAB reference cannot run here and ships no tests or golden vectors
+(SURVEY.md §4), so the oracle is pinned by invariants derived from the
+reference's own code, each test citing the lines it follows, plus
+50-digit KKT certificates for the QP (quadprog itself is unavailable:
+"parity unpinned" against quadprog, pinned against the exact optimum).
+"""
+import itertools
+import math
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oracle import ntm_oracle as O
+
+GOLD = Path(__file__).resolve().parent / "golden"
+PH = O.Physics()
+
+
+def cfg(N=3, mode=O.MODE_FULL, **kw):
+    return O.Config(N=N, mode=mode, **kw)
+
+
+def rand_rho(N, seed=0):
+    rng = np.random.default_rng(seed)
+    c = cfg(N)
+    xs = np.stack([rng.uniform(0.06, 0.15, N), rng.uniform(0.8, 1.2, N) * 2000 * math.pi])
+    return np.stack([O.rho_all(xs[:, i], PH, c) for i in range(N)], axis=1)
+
+
+# ------------------------------------------------------------------ constants
+def test_derived_constants():
+    """NTM_MPC_Sim.m:24-25, 37 (values quoted in SURVEY.md App. A)."""
+    assert PH.kappa() == pytest.approx(5.7400e-8, rel=1e-3)
+    assert PH.zeta() == pytest.approx(2.7072e-11, rel=1e-4)
+    C = O.C_vec(PH, 0.1)
+    assert C[0] == pytest.approx(-1.7391e-3, rel=1e-4)
+    assert C[1] == pytest.approx(71.3226, rel=1e-5)
+    A = O.A_mat(*O.rho_all(np.array([0.1, 2000 * math.pi]), PH, cfg())[:2], PH, 0.1)
+    assert A[1, 0] == pytest.approx(734.9, rel=1e-3)
+    assert A[1, 1] == pytest.approx(1 - 0.1 / 3.7)
+
+
+def test_rho_functions_match_reference_formulas():
+    """rho1.m:2 (unsquared w, D18), rho2.m:2, rho3.m:2-3."""
+    x = np.array([0.1, 5000.0])
+    assert O.rho1(x, 0.02) == 1 / (0.1 + 0.02 ** 2)
+    assert O.rho1(x, 0.02, squared=True) == 1 / (0.1 ** 2 + 0.02 ** 2)
+    assert O.rho2(x) == 0.1 ** 2 / 5000.0
+    ws = 0.1 / 0.024
+    assert O.rho3(x, 0.024) == pytest.approx((0.25 + 0.24 * ws) / (1 + 1.5 * ws + 0.43 * ws ** 2 + 0.64 * ws ** 3),
+                                             rel=1e-15)
+
+
+# ------------------------------------------------------------------ lift
+@pytest.mark.parametrize("N", [1, 2, 5, 20])
+def test_rollout_identity(N):
+    """CANON D4/D6: X = Phi x0 + Gamma U + Lambda equals the step-by-step model of
+    NTM_MPC_Sim.m:113 (x_{i} = A_i x_{i-1} + B_i u_i + C) for any U."""
+    c = cfg(N)
+    Rho = rand_rho(N, N)
+    Phi, Gam, Lam = O.lift(Rho, PH, c)
+    rng = np.random.default_rng(7)
+    x0 = np.array([0.1, 6000.0])
+    U = rng.uniform(0, 2e6, N)
+    X = Phi @ x0 + Gam @ U + Lam
+    x = x0.copy()
+    Cv = O.C_vec(PH, c.Ts)
+    for i in range(N):
+        x = O.A_mat(Rho[0, i], Rho[1, i], PH, c.Ts) @ x + O.B_mat(Rho[2, i], PH, c.Ts) * U[i] + Cv
+        np.testing.assert_allclose(X[2 * i:2 * i + 2], x, rtol=1e-13)
+
+
+def test_lti_closed_forms():
+    """Constant rho: Phi_i = A^i, Gamma_ij = A^(i-j) B, Lambda_i = sum_{k<i} A^k C."""
+    N = 6
+    c = cfg(N)
+    r = O.rho_all(np.array([0.1, 6000.0]), PH, c)
+    Rho = np.tile(r[:, None], (1, N))
+    Phi, Gam, Lam = O.lift(Rho, PH, c)
+    A = O.A_mat(r[0], r[1], PH, c.Ts)
+    B = O.B_mat(r[2], PH, c.Ts)
+    Cv = O.C_vec(PH, c.Ts)
+    for i in range(1, N + 1):
+        np.testing.assert_allclose(Phi[2 * i - 2:2 * i], np.linalg.matrix_power(A, i), rtol=1e-13)
+        np.testing.assert_allclose(Lam[2 * i - 2:2 * i], sum(np.linalg.matrix_power(A, k) @ Cv for k in range(i)),
+                                   rtol=1e-13)
+        for j in range(1, i + 1):
+            np.testing.assert_allclose(Gam[2 * i - 2:2 * i, j - 1], np.linalg.matrix_power(A, i - j) @ B, rtol=1e-13)
+
+
+def test_literal_switches_agree_for_lti_only():
+    """D4 / D6: the literal index/product order equals CANON for constant rho
+     and differs once rho varies."""
+    N = 5
+    r = O.rho_all(np.array([0.1, 6000.0]), PH, cfg(N))
+    Rho = np.tile(r[:, None], (1, N))
+    lit = cfg(N, flags=O.LITERAL_GAMMA_INDEX)
+    _, G1, _ = O.lift(Rho, PH, cfg(N))
+    _, G2, _ = O.lift(Rho, PH, lit)
+    np.testing.assert_allclose(G1, G2, rtol=1e-14)
+    Rv = rand_rho(N, 3)
+    _, G1, _ = O.lift(Rv, PH, cfg(N))
+    _, G2, _ = O.lift(Rv, PH, lit)
+    assert np.max(np.abs(G1 - G2)) > 0
+
+
+# ------------------------------------------------------------------ getWLc
+@pytest.mark.parametrize("N", [1, 3, 8])
+def test_getwlc_equals_per_step_constraints(N):
+    """getWLc.m:9-26: L U <= c + W x0 row by row equals the per-step box
+    constraints u_i in [umin, umax] (i=0..N-1), x_i in [xmin, xmax] (i=0..N)."""
+    c = cfg(N)
+    Rho = rand_rho(N, 11)
+    Phi, Gam, Lam = O.lift(Rho, PH, c)
+    W, L, cv = O.getWLc(c.xmax, c.xmin, c.umax, c.umin, Gam, Phi, Lam)
+    assert L.shape == (6 * N + 4, N) and W.shape == (6 * N + 4, 2)
+    rng = np.random.default_rng(5)
+    x0 = np.array([0.1, 6000.0])
+    U = rng.uniform(-1e6, 3e6, N)
+    lhs = L @ U - (cv + W @ x0)
+    X = np.concatenate([x0, Phi @ x0 + Gam @ U + Lam])
+    expect = []
+    for i in range(N + 1):
+        xi = X[2 * i:2 * i + 2]
+        if i < N:
+            expect += [-U[i] + c.umin, U[i] - c.umax]
+        expect += [-xi[0] + c.xmin[0], -xi[1] + c.xmin[1], xi[0] - c.xmax[0], xi[1] - c.xmax[1]]
+    np.testing.assert_allclose(lhs, np.array(expect), rtol=1e-10, atol=1e-9)
+
+
+def test_reference_x0_is_infeasible():
+    """Known answer (D15): x0 = [0; 2000 pi] (NTM_MPC_Sim.m:34) violates w >= 0.06
+    (:40): the constant k=0 row reads 0 <= -0.06, so quadprog returns -2 (:100)."""
+    c = cfg(3)
+    x0 = O.REFERENCE_X0
+    Rho = O.initial_rho(x0, PH, c)
+    Phi, Gam, Lam = O.lift(Rho, PH, c)
+    G, F = O.cost(Phi, Gam, Lam, x0, c)
+    Lin, b = O.constraints(Phi, Gam, Lam, x0, c)
+    assert np.all(Lin[2] == 0) and b[2] == pytest.approx(-0.06)
+    U, flag, _ = O.qp_solve(G, F, Lin, b)
+    assert flag == O.EXIT_INFEASIBLE and np.all(U == 0)
+    st = O.mpc_step(x0, Rho, np.full(3, np.inf), PH, c)
+    assert st["exitflag"] == -2 and st["u"] == 0
+
+
+# ------------------------------------------------------------------ QP
+def _brute_force_qp(G, F, Lin, b, max_active):
+    """Enumerate active sets (<= max_active rows), keep the feasible KKT point."""
+    n = G.shape[0]
+    best = None
+    nz = [i for i in range(Lin.shape[0]) if np.any(Lin[i] != 0)]
+    for k in range(0, max_active + 1):
+        for A in itertools.combinations(nz, k):
+            A = list(A)
+            K = np.block([[G, Lin[A].T], [Lin[A], np.zeros((k, k))]]) if k else G
+            rhs = np.concatenate([-F, b[A]]) if k else -F
+            try:
+                sol = np.linalg.solve(K, rhs)
+            except np.linalg.LinAlgError:
+                continue
+            U, lam = sol[:n], sol[n:]
+            if np.all(lam >= -1e-9 * max(1, np.max(np.abs(lam), initial=1))) and \
+                    np.all(Lin @ U <= b + 1e-7 * np.maximum(1, np.abs(b))):
+                f = 0.5 * U @ G @ U + F @ U
+                if best is None or f < best[0] - 1e-12 * abs(f):
+                    best = (f, U)
+    return best
+
+
+def test_qp_matches_active_set_enumeration():
+    """N=3 problems from closed-loop states: the dual active-set result equals the
+    exhaustive active-set enumeration (the optimum is unique: G > 0)."""
+    c = cfg(3)
+    x0s = O.scenario_x0(np.arange(6))
+    checked = 0
+    for s in range(6):
+        x = x0s[s]
+        Rho = O.initial_rho(x, PH, c)
+        Phi, Gam, Lam = O.lift(Rho, PH, c)
+        G, F = O.cost(Phi, Gam, Lam, x, c)
+        Lin, b = O.constraints(Phi, Gam, Lam, x, c)
+        U, flag, _ = O.qp_solve(G, F, Lin, b)
+        if flag != 1:
+            continue
+        best = _brute_force_qp(G, F, Lin, b, 3)
+        assert best is not None
+        assert np.max(np.abs(U - best[1])) / c.umax <= 1e-9
+        checked += 1
+    assert checked >= 4
+
+
+def test_qp_golden_certified():
+    """Committed QPs (N=20) with 50-digit-certified optima: the oracle's fp64
+    solution is within 1e-11 * umax of the exact KKT point."""
+    for name in ("qp_m2_N20.npz", "qp_m1_N20.npz"):
+        d = np.load(GOLD / name)
+        for i in range(d["G"].shape[0]):
+            U, flag, info = O.qp_solve(d["G"][i], d["F"][i], d["Lin"][i], d["b"][i])
+            assert flag == d["exitflag"][i]
+            assert info["polished"]
+            assert np.max(np.abs(U - d["U_exact"][i])) / 2e6 <= 1e-11
+
+
+def test_kkt_certificate_50_digits():
+    d = np.load(GOLD / "qp_m2_N20.npz")
+    for i in range(3):
+        U, flag, info = O.qp_solve(d["G"][i], d["F"][i], d["Lin"][i], d["b"][i])
+        Ue, lam, cert = O.kkt_polish(d["G"][i], d["F"][i], d["Lin"][i], d["b"][i], info["active"], dps=50)
+        assert cert["max_violation"] <= 1e-12 and cert["min_multiplier"] >= -1e-12
+
+
+def test_unconstrained_lq_vs_mpmath():
+    """BASELINE config 1 (N=10, reference x0, no constraints): U = -G^{-1} F in
+    fp64 agrees with a 50-digit solve."""
+    import mpmath as mp
+    c = cfg(10, O.MODE_NONE)
+    x0 = O.REFERENCE_X0
+    Rho = O.initial_rho(x0, PH, c)
+    Phi, Gam, Lam = O.lift(Rho, PH, c)
+    G, F = O.cost(Phi, Gam, Lam, x0, c)
+    U, flag, _ = O.qp_solve(G, F, np.zeros((0, 10)), np.zeros(0))
+    with mp.workdps(50):
+        Ue = mp.lu_solve(mp.matrix([[mp.mpf(float(v)) for v in row] for row in G]),
+                         mp.matrix([-mp.mpf(float(v)) for v in F]))
+        Ue = np.array([float(v) for v in Ue])
+    assert flag == 1
+    assert np.max(np.abs(U - Ue)) <= 1e-10 * np.max(np.abs(Ue))
+
+
+# ------------------------------------------------------------------ closed loop
+@pytest.mark.parametrize("name", ["closed_loop_m0_N10.npz", "closed_loop_m2_N3.npz"])
+def test_closed_loop_golden(name):
+    """Regression pin: the oracle reproduces its committed closed-loop fixtures."""
+    d = np.load(GOLD / name)
+    mode = int(name.split("_m")[1][0])
+    N = int(name.split("_N")[1].split(".")[0])
+    c = cfg(N, mode)
+    for s in range(d["x0"].shape[0]):
+        out = O.closed_loop(d["x0"][s], PH, c, int(d["k_sim"]))
+        np.testing.assert_array_equal(out["exitflag"], d["exitflag"][s])
+        np.testing.assert_allclose(out["uk"], d["uk"][s], rtol=0, atol=1e-9 * c.umax)
+        np.testing.assert_allclose(out["xk"], d["xk"][s], rtol=1e-9, atol=1e-15)
+
+
+def test_lpv_loop_semantics():
+    """NTM_MPC_Sim.m:94-127: the LPV loop runs at most i_sim QPs, stops when
+    sum|U - Uold| < eps, carries rho unshifted (D20) and Uold across steps (D14),
+    and the applied input is U(1) of the last QP (D21)."""
+    c = cfg(3)
+    x0 = O.scenario_x0([0])[0]
+    Rho = O.initial_rho(x0, PH, c)
+    st = O.mpc_step(x0, Rho, np.full(3, np.inf), PH, c)
+    assert 1 <= st["inner_iters"] <= c.i_sim
+    assert st["u"] == st["U"][0]
+    np.testing.assert_array_equal(st["Uold"], st["U"])
+    xp, Rn = O.rollout(x0, Rho, st["U"], PH, c)        # rho_i <- rho(x_{i-1})
+    np.testing.assert_allclose(Rn[:, 0], O.rho_all(x0, PH, c))
+    c1 = cfg(3, i_sim=1)
+    assert O.mpc_step(x0, Rho, np.full(3, np.inf), PH, c1)["inner_iters"] == 1
+
+
+def test_plant_step_literal_switch():
+    """D13: CANON plant = prediction model (+C); LITERAL drops C (NTM_MPC_Sim.m:130)."""
+    x = np.array([0.1, 6000.0])
+    a = O.plant_step(x, 1e6, PH, cfg())
+    b = O.plant_step(x, 1e6, PH, cfg(flags=O.LITERAL_PLANT_NO_C))
+    np.testing.assert_allclose(a - b, O.C_vec(PH, 0.1), rtol=1e-12)
+
+
+def test_scenario_generator_ranges():
+    x = O.scenario_x0(np.arange(1000))
+    assert np.all((x[:, 0] >= 0.07) & (x[:, 0] < 0.14))
+    assert np.all((x[:, 1] >= 0.8 * 2000 * math.pi) & (x[:, 1] < 1.2 * 2000 * math.pi))
+    np.testing.assert_array_equal(O.scenario_x0([5, 6]), x[5:7])     # counter-based: shard invariant
