@@ -88,6 +88,9 @@ const char* ntm_last_error(const ntm_ctx* ctx);
  * step/run launches ACCUMULATE into: QP solves, Goldfarb-Idnani iterations,
  * final active rows, general (state) active rows.  NULL disables. */
 int ntm_ctx_set_stats(ntm_ctx* ctx, int32_t* dev_stats);
+/* Diagnostic builds only: per-phase s_memtime cycle totals (16 counters);
+ * NTM_E_UNSUPPORTED in production builds. */
+int ntm_debug_stamps(unsigned long long* out16, int reset);
 
 /* ---- time-step level: the drop-in for NTM_MPC_Sim.m:94-130 ------------ */
 /* One MPC step for B scenarios.  In/out state per scenario:

@@ -47,6 +47,35 @@ struct Prob {
 };
 
 constexpr double kInf = __builtin_huge_val();
+
+// Diagnostic build only (-DNTM_STAMPS): per-phase s_memtime cycle totals,
+// summed over waves into ntm_stamps[] (read with ntm_debug_stamps).  The
+// production library compiles every stamp away.
+#ifdef NTM_STAMPS
+extern __device__ unsigned long long ntm_stamps[16];
+__shared__ unsigned long long ntm_lds_stamps[16];   // per block (= per wave), flushed once
+#define NTM_T0(v) unsigned long long v = __builtin_amdgcn_s_memtime()
+#define NTM_ACC(i, v)                                                                   \
+    do {                                                                                \
+        unsigned long long t1_ = __builtin_amdgcn_s_memtime();                         \
+        if ((threadIdx.x & 63) == 0) ntm_lds_stamps[i] += t1_ - (v);                   \
+        v = t1_;                                                                        \
+    } while (0)
+#define NTM_CNT(i) \
+    do { if ((threadIdx.x & 63) == 0) ntm_lds_stamps[i] += 1ull; } while (0)
+#define NTM_STAMPS_INIT() \
+    do { if (threadIdx.x < 16) ntm_lds_stamps[threadIdx.x] = 0; __syncthreads(); } while (0)
+#define NTM_STAMPS_FLUSH() \
+    do { __syncthreads(); if (threadIdx.x < 16) atomicAdd(&ntm_stamps[threadIdx.x], ntm_lds_stamps[threadIdx.x]); } while (0)
+#else
+#define NTM_T0(v) (void)0
+#define NTM_ACC(i, v) (void)0
+#define NTM_CNT(i) (void)0
+#define NTM_STAMPS_INIT() (void)0
+#define NTM_STAMPS_FLUSH() (void)0
+#endif
+enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL, ST_GI_FACT, ST_GI_CHECK,
+       ST_GI_DIR, ST_GI_ADD, ST_GI_DROP, CN_CHECK, CN_CAND, CN_HIT };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 
 #define NTM_WSYNC()                                              \
@@ -105,6 +134,25 @@ __device__ __forceinline__ void pair_i(int v, int& lo, int& hi) {
     }
 }
 
+// P = 64 (one scenario per wave): results of group reductions are identical
+// in every lane; readfirstlane makes that visible to the compiler, so the
+// branches they feed become scalar branches and loop counters live in SGPRs.
+template <int P>
+__device__ __forceinline__ int uni(int v) {
+    if constexpr (P == 64) return __builtin_amdgcn_readfirstlane(v);
+    else return v;
+}
+template <int P>
+__device__ __forceinline__ double uni(double v) {
+    if constexpr (P == 64) {
+        int2 a = __builtin_bit_cast(int2, v);
+        a.x = __builtin_amdgcn_readfirstlane(a.x);
+        a.y = __builtin_amdgcn_readfirstlane(a.y);
+        return __builtin_bit_cast(double, a);
+    } else {
+        return v;
+    }
+}
 template <int P>
 __device__ __forceinline__ double gsum(double v) {
     v = v + dpp_d<0xB1>(v);                       // quad_perm [1,0,3,2]
@@ -113,7 +161,7 @@ __device__ __forceinline__ double gsum(double v) {
     if constexpr (P >= 16) v = v + dpp_d<0x140>(v);  // row_mirror
     if constexpr (P >= 32) { double a, b; pair_d<16>(v, a, b); v = a + b; }
     if constexpr (P >= 64) { double a, b; pair_d<32>(v, a, b); v = a + b; }
-    return v;
+    return uni<P>(v);
 }
 template <int P>
 __device__ __forceinline__ double gmax(double v) {
@@ -123,7 +171,7 @@ __device__ __forceinline__ double gmax(double v) {
     if constexpr (P >= 16) v = fmax(v, dpp_d<0x140>(v));
     if constexpr (P >= 32) { double a, b; pair_d<16>(v, a, b); v = fmax(a, b); }
     if constexpr (P >= 64) { double a, b; pair_d<32>(v, a, b); v = fmax(a, b); }
-    return v;
+    return uni<P>(v);
 }
 template <int P>
 __device__ __forceinline__ int gmaxi(int v) {
@@ -133,10 +181,20 @@ __device__ __forceinline__ int gmaxi(int v) {
     if constexpr (P >= 16) v = max(v, dpp_i<0x140>(v));
     if constexpr (P >= 32) { int a, b; pair_i<16>(v, a, b); v = max(a, b); }
     if constexpr (P >= 64) { int a, b; pair_i<32>(v, a, b); v = max(a, b); }
-    return v;
+    return uni<P>(v);
 }
+// broadcast lane `src` of the group (src group-uniform)
 template <int P>
-__device__ __forceinline__ double gbcast(double v, int src) { return __shfl(v, src, P); }
+__device__ __forceinline__ double gbcast(double v, int src) {
+    if constexpr (P == 64) {
+        int2 a = __builtin_bit_cast(int2, v);
+        a.x = __builtin_amdgcn_readlane(a.x, src);
+        a.y = __builtin_amdgcn_readlane(a.y, src);
+        return __builtin_bit_cast(double, a);
+    } else {
+        return __shfl(v, src, P);
+    }
+}
 
 // argmin over (v, id) with ties broken towards the smaller id; carries two
 // payload doubles.  Identical result in every lane of the group.
@@ -167,6 +225,10 @@ __device__ __forceinline__ void gargmin(double& v, int& id, double& a, double& b
     if constexpr (P >= 16) amin_dpp<0x140>(v, id, a, b);
     if constexpr (P >= 32) amin_pair<16>(v, id, a, b);
     if constexpr (P >= 64) amin_pair<32>(v, id, a, b);
+    v = uni<P>(v);
+    id = uni<P>(id);
+    a = uni<P>(a);
+    b = uni<P>(b);
 }
 template <int P>
 __device__ __forceinline__ void gargmin(double& v, int& id) {
@@ -193,59 +255,79 @@ __device__ __forceinline__ double coef_b(const Coef& k, double r3) { return k.bc
 // ---------------------------------------------------------------------------
 // per-scenario LDS workspace (all offsets in doubles; see ws_doubles())
 // ---------------------------------------------------------------------------
+// NN > 0: horizon fixed at compile time (strides become immediates, loops
+// unroll); NN == 0: runtime horizon (generic kernels).
+template <int NN>
 struct WS {
-    int N, LDG, LDJ;
+    int N_rt;
     double* base;
-    // double offsets of each array (N is launch-uniform, so these fold to scalar math)
-    __device__ __forceinline__ int oJ() const { return 14 * N + 2 * N * N; }
-    __device__ __forceinline__ int oR() const { return oJ() + N * LDJ; }
-    __device__ __forceinline__ int oM() const { return oR() + N * LDJ; }
-    __device__ __forceinline__ int oV() const { return oM() + N * LDJ; }   // start of the vector block
+    __device__ __forceinline__ int n() const { return NN > 0 ? NN : N_rt; }
+    __device__ __forceinline__ int ldj() const { return n() | 1; }
+    __device__ __forceinline__ int ldg() const { return 2 * n(); }
+    // double offsets of each array (n() is launch-uniform, so these fold to scalar math)
+    __device__ __forceinline__ int oJ() const { return 14 * n() + n() * (n() + 1); }
+    __device__ __forceinline__ int oR() const { return oJ() + n() * ldj(); }
+    __device__ __forceinline__ int oV() const { return oR() + (n() + 1) * ldj(); }   // start of the vector block
     __device__ __forceinline__ double* rho() const { return base; }                 // 3N (3xN col-major)
-    __device__ __forceinline__ double* a11() const { return base + 3 * N; }         // N
-    __device__ __forceinline__ double* a21() const { return base + 4 * N; }         // N
-    __device__ __forceinline__ double* bb() const { return base + 5 * N; }          // N
-    __device__ __forceinline__ double* Phi() const { return base + 6 * N; }         // 4N Phi_i (2x2 col-major)
-    __device__ __forceinline__ double* Lam() const { return base + 10 * N; }        // 2N
-    __device__ __forceinline__ double* e() const { return base + 12 * N; }          // 2N free response
-    __device__ __forceinline__ double* Gt() const { return base + 14 * N; }         // 2N x N col-major Gamma
-    __device__ __forceinline__ double* J() const { return base + oJ(); }            // N x LDJ row-major
-    __device__ __forceinline__ double* R() const { return base + oR(); }            // N x LDJ col-major
-    __device__ __forceinline__ double* M() const { return base + oM(); }            // N x LDJ col-major
+    __device__ __forceinline__ double* a11() const { return base + 3 * n(); }         // n()
+    __device__ __forceinline__ double* a21() const { return base + 4 * n(); }         // n()
+    __device__ __forceinline__ double* bb() const { return base + 5 * n(); }          // n()
+    __device__ __forceinline__ double* Phi() const { return base + 6 * n(); }         // 4N Phi_i (2x2 col-major)
+    __device__ __forceinline__ double* Lam() const { return base + 10 * n(); }        // 2N
+    __device__ __forceinline__ double* e() const { return base + 12 * n(); }          // 2N free response
+    // Gamma, block-lower-triangular and packed by column: column j holds rows 2j..2N-1
+    __device__ __forceinline__ double* Gt() const { return base + 14 * n(); }         // n()(n()+1)
+    __device__ __forceinline__ int gidx(int r, int j) const { return j * (2 * n() - j + 1) + r - 2 * j; }
+    __device__ __forceinline__ double& gt(int r, int j) const { return Gt()[gidx(r, j)]; }   // r >= 2j
+    __device__ __forceinline__ double* J() const { return base + oJ(); }            // n() x ldj() row-major
+    // R: n() rows x (n()+1) columns col-major; the polish keeps its Schur complement
+    // K in the strict upper triangle: K(a, c), a >= c, at R[c + (a+1) ldj()]
+    __device__ __forceinline__ double* R() const { return base + oR(); }
     __device__ __forceinline__ double* rn() const { return base + oV(); }           // 2N state-row norms
-    __device__ __forceinline__ double* F() const { return base + oV() + 2 * N; }    // N  F~
-    __device__ __forceinline__ double* D() const { return base + oV() + 3 * N; }    // N  Jacobi scaling
-    __device__ __forceinline__ double* V() const { return base + oV() + 4 * N; }    // N  scaled variables
-    __device__ __forceinline__ double* d() const { return base + oV() + 5 * N; }    // N
-    __device__ __forceinline__ double* np() const { return base + oV() + 6 * N; }   // N  GI normal
-    __device__ __forceinline__ double* hv() const { return base + oV() + 7 * N; }   // N  Householder / polish
-    __device__ __forceinline__ double* Vb() const { return base + oV() + 8 * N; }   // N  polish fixed (V)
-    __device__ __forceinline__ double* Uf() const { return base + oV() + 9 * N; }   // N  polish fixed (U)
-    __device__ __forceinline__ double* uu() const { return base + oV() + 10 * N; }  // N+1 multipliers
-    __device__ __forceinline__ double* xp() const { return base + oV() + 11 * N + 1; }   // 2(N+1) rollout
-    __device__ __forceinline__ double* U() const { return base + oV() + 13 * N + 3; }    // N
-    __device__ __forceinline__ double* Uold() const { return base + oV() + 14 * N + 3; } // N
-    __device__ __forceinline__ int* act() const { return reinterpret_cast<int*>(base + oV() + 15 * N + 3); }
-    __device__ __forceinline__ int* sidx() const { return act() + N + 1; }
-    __device__ __forceinline__ int* cand() const { return act() + 2 * (N + 1); }   // 2(N+1): last two active sets
+    __device__ __forceinline__ double* F() const { return base + oV() + 2 * n(); }    // n()  F~
+    __device__ __forceinline__ double* D() const { return base + oV() + 3 * n(); }    // n()  Jacobi scaling
+    __device__ __forceinline__ double* V() const { return base + oV() + 4 * n(); }    // n()  scaled variables
+    __device__ __forceinline__ double* d() const { return base + oV() + 5 * n(); }    // n()
+    __device__ __forceinline__ double* np() const { return base + oV() + 6 * n(); }   // n()  GI normal
+    __device__ __forceinline__ double* hv() const { return base + oV() + 7 * n(); }   // n()  Householder / polish
+    __device__ __forceinline__ double* Vb() const { return base + oV() + 8 * n(); }   // n()  polish fixed (V)
+    __device__ __forceinline__ double* Uf() const { return base + oV() + 9 * n(); }   // n()  polish fixed (U)
+    __device__ __forceinline__ double* uu() const { return base + oV() + 10 * n(); }  // n()+1 multipliers
+    __device__ __forceinline__ double* xp() const { return base + oV() + 11 * n() + 1; }   // 2(n()+1) rollout
+    __device__ __forceinline__ double* U() const { return base + oV() + 13 * n() + 3; }    // n()
+    __device__ __forceinline__ double* Uold() const { return base + oV() + 14 * n() + 3; } // n()
+    __device__ __forceinline__ double* rinv() const { return base + oV() + 15 * n() + 3; }  // N: 1/R(b,b) of the GI R
+    // per-QP constants hoisted out of the solver loops
+    __device__ __forceinline__ double* vlo() const { return base + oV() + 16 * n() + 3; }   // N: umin/D_j
+    __device__ __forceinline__ double* vhi() const { return base + oV() + 17 * n() + 3; }   // N: umax/D_j
+    __device__ __forceinline__ double* irn() const { return base + oV() + 18 * n() + 3; }   // 2N: 1/rn_r (0: const row)
+    __device__ __forceinline__ double* ldi() const { return base + oV() + 20 * n() + 3; }   // N: 1/L(k,k) (Cholesky)
+    __device__ __forceinline__ double* kdi() const { return base + oV() + 21 * n() + 3; }   // N: 1/K(k,k) (Schur)
+    __device__ __forceinline__ double* ssg() const { return base + oV() + 22 * n() + 3; }   // N: sign of general row s
+    __device__ __forceinline__ int* act() const { return reinterpret_cast<int*>(base + oV() + 23 * n() + 3); }
+    __device__ __forceinline__ int* sidx() const { return act() + n() + 1; }
+    __device__ __forceinline__ int* cand() const { return act() + 2 * (n() + 1); }   // 2(n()+1): last two active sets
+    __device__ __forceinline__ int* fidx() const { return act() + 4 * (n() + 1); }   // n()+1: free variables (polish)
+    __device__ __forceinline__ int* srw() const { return act() + 5 * (n() + 1); }    // n()+1: state row of general row s
     __device__ __forceinline__ unsigned char* fx() const {
-        return reinterpret_cast<unsigned char*>(act() + 4 * (N + 1));
+        return reinterpret_cast<unsigned char*>(act() + 6 * (n() + 1));
     }
-    __device__ __forceinline__ unsigned char* aflag() const { return fx() + N; }
+    __device__ __forceinline__ unsigned char* aflag() const { return fx() + n(); }
 };
 
 __host__ __device__ inline int ldj_of(int N) { return N | 1; }
-__host__ __device__ inline int ws_doubles(int N) { return 14 * N + 2 * N * N + 3 * N * ldj_of(N) + 15 * N + 3; }
+__host__ __device__ inline int ws_doubles(int N) {
+    return 14 * N + N * (N + 1) + N * ldj_of(N) + (N + 1) * ldj_of(N) + 23 * N + 3;
+}
 __host__ __device__ inline int ws_bytes(int N) {
-    int b = ws_doubles(N) * 8 + 4 * (N + 1) * 4 + N + (6 * NTM_MAX_N + 4);
+    int b = ws_doubles(N) * 8 + 6 * (N + 1) * 4 + N + (6 * NTM_MAX_N + 4);
     return (b + 15) & ~15;
 }
 
-__device__ inline WS ws_carve(char* base, int N) {
-    WS w;
-    w.N = N;
-    w.LDG = 2 * N;
-    w.LDJ = ldj_of(N);
+template <int NN>
+__device__ inline WS<NN> ws_carve(char* base, int N) {
+    WS<NN> w;
+    w.N_rt = N;
     w.base = reinterpret_cast<double*>(base);
     return w;
 }
@@ -253,9 +335,9 @@ __device__ inline WS ws_carve(char* base, int N) {
 // ---------------------------------------------------------------------------
 // L2: lifted prediction  (Rho_to_PhiGammaLambda.m:17-52, CANON D4/D6)
 // ---------------------------------------------------------------------------
-template <int P>
-__device__ void lift_phase(const Prob& pb, const WS& w, int l) {
-    const int N = w.N;
+template <int P, class W>
+__device__ void lift_phase(const Prob& pb, const W& w, int l) {
+    const int N = w.n();
     const Coef& k = pb.k;
     if (l < N) {
         w.a11()[l] = coef_a11(k, w.rho()[3 * l]);
@@ -265,8 +347,7 @@ __device__ void lift_phase(const Prob& pb, const WS& w, int l) {
     NTM_WSYNC();
     // Gamma: lane j owns column j: Gamma_jj = B_j, Gamma_ij = A_i Gamma_{i-1,j} (D6)
     if (l < N) {
-        double* col = w.Gt() + l * w.LDG;
-        for (int r = 0; r < 2 * l; ++r) col[r] = 0.0;
+        double* col = w.Gt() + w.gidx(2 * l, l) - 2 * l;   // col[r], r >= 2l
         double g0 = w.bb()[l], g1 = 0.0;
         col[2 * l] = g0;
         col[2 * l + 1] = g1;
@@ -302,9 +383,9 @@ __device__ void lift_phase(const Prob& pb, const WS& w, int l) {
 
 // free response e = Phi x_k + Lambda (the x-dependent part of NTM_MPC_Sim.m:121
 // and of c + W x_k at :97)
-template <int P>
-__device__ void free_response(const WS& w, double x0, double x1, int l) {
-    for (int i = l; i < w.N; i += P) {
+template <int P, class W>
+__device__ void free_response(const W& w, double x0, double x1, int l) {
+    for (int i = l; i < w.n(); i += P) {
         const double* Ph = w.Phi() + 4 * i;
         w.e()[2 * i] = (Ph[0] * x0 + Ph[2] * x1) + w.Lam()[2 * i];
         w.e()[2 * i + 1] = (Ph[1] * x0 + Ph[3] * x1) + w.Lam()[2 * i + 1];
@@ -316,14 +397,14 @@ __device__ void free_response(const WS& w, double x0, double x1, int l) {
 // condensed cost G = 2 Gamma' Om Gamma (lower triangle into dst, col-major),
 // F = 2 Gamma' Om (e - R)      NTM_MPC_Sim.m:120-121 (CANON D8, D12)
 // ---------------------------------------------------------------------------
-template <int P>
-__device__ void gram_rows(const Prob& pb, const WS& w, double* dst, int l) {
-    const int N = w.N, LD = w.LDJ, LDG = w.LDG;
+template <int P, class W>
+__device__ void gram_rows(const Prob& pb, const W& w, double* dst, int l) {
+    const int N = w.n(), LD = w.ldj();
     const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
     if (l < N) {
-        const double* cj = w.Gt() + l * LDG;
+        const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
         for (int kk = 0; kk <= l; ++kk) {
-            const double* ck = w.Gt() + kk * LDG;
+            const double* ck = w.Gt() + w.gidx(2 * kk, kk) - 2 * kk;
             double s = 0.0;
             for (int i = l; i < N; ++i) {
                 double g0 = ck[2 * i], g1 = ck[2 * i + 1];
@@ -337,13 +418,13 @@ __device__ void gram_rows(const Prob& pb, const WS& w, double* dst, int l) {
     }
 }
 
-template <int P>
-__device__ void cost_phase(const Prob& pb, const WS& w, int l) {
-    const int N = w.N, LDG = w.LDG;
+template <int P, class W>
+__device__ void cost_phase(const Prob& pb, const W& w, int l) {
+    const int N = w.n();
     const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
     gram_rows<P>(pb, w, w.R(), l);
     if (l < N) {
-        const double* cj = w.Gt() + l * LDG;
+        const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
         double f = 0.0;
         for (int i = l; i < N; ++i) {
             double e0 = w.e()[2 * i] - pb.r[0], e1 = w.e()[2 * i + 1] - pb.r[1];
@@ -358,28 +439,85 @@ __device__ void cost_phase(const Prob& pb, const WS& w, int l) {
 
 // G~ = D G D in place (lower triangle, col-major); the same expression order
 // is used when the polish recomputes G~ (so both copies are bit-identical).
-template <int P>
-__device__ int scale_gram(const WS& w, double* G, int l) {
+template <int P, class W>
+__device__ int scale_gram(const W& w, double* G, int l) {
     int bad = 0;
-    if (l < w.N) {
+    if (l < w.n()) {
         double Dl = w.D()[l];
         for (int kk = 0; kk <= l; ++kk) {
-            double v = G[l + kk * w.LDJ] * Dl * w.D()[kk];
+            double v = G[l + kk * w.ldj()] * Dl * w.D()[kk];
             bad |= !isfinite(v);
-            G[l + kk * w.LDJ] = v;
+            G[l + kk * w.ldj()] = v;
         }
     }
     return bad;
 }
 
 // ---------------------------------------------------------------------------
-// Jacobi scaling U = D V: G~ = D G D, F~ = D F, norms of the scaled state rows
-// ||Gamma_r D||.  Gamma itself stays unscaled (D is applied on the fly).
+// Jacobi scaling U = D V with D = diag(G)^{-1/2}, computed from the Gram
+// diagonal only (same summation order as gram_rows, so D is bit-identical to
+// what the full G would give); F~ = D F; norms of the scaled state rows
+// ||Gamma_r D||.  Gamma stays unscaled (D is applied on the fly).  The full
+// G~ is only formed when the Goldfarb-Idnani fallback runs (full_gram).
 // Returns false (group-uniform) if any datum is non-finite.
 // ---------------------------------------------------------------------------
-template <int P>
-__device__ bool scale_phase(const WS& w, int l, bool with_state_rows) {
-    const int N = w.N, LD = w.LDJ, LDG = w.LDG;
+template <int P, class W>
+__device__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_state_rows) {
+    const int N = w.n();
+    const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
+    int bad = 0;
+    if (l < N) {
+        const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
+        double s = 0.0;
+        for (int i = l; i < N; ++i) {
+            double g0 = cj[2 * i], g1 = cj[2 * i + 1];
+            bad |= !isfinite(g0) || !isfinite(g1);
+            double o0 = q00 * g0 + q01 * g1;
+            double o1 = q10 * g0 + q11 * g1;
+            s += g0 * o0;
+            s += g1 * o1;
+        }
+        double g = 2 * s;
+        double Dl = (g > 0.0) ? 1.0 / sqrt(g) : 1.0;
+        w.D()[l] = Dl;
+        double f = w.F()[l] * Dl;
+        bad |= !isfinite(f) || !isfinite(Dl);
+        w.F()[l] = f;
+        // V-space box of u_l (bc of the two u rows; same expressions as the oracle's b/rn)
+        w.vlo()[l] = -((-pb.umin) / Dl);
+        w.vhi()[l] = pb.umax / Dl;
+    }
+    NTM_WSYNC();
+    if (with_state_rows) {
+        for (int r = l; r < 2 * N; r += P) {
+            double s = 0.0;
+            int jmax = r >> 1;
+            for (int j = 0; j <= jmax; ++j) { double v = w.gt(r, j) * w.D()[j]; s += v * v; }
+            bad |= !isfinite(s) || !isfinite(w.e()[r]);
+            double rn = s > 0.0 ? sqrt(s) : 0.0;
+            w.rn()[r] = rn;
+            w.irn()[r] = rn > 0.0 ? 1.0 / rn : 0.0;
+        }
+        NTM_WSYNC();
+    }
+    return gmaxi<P>(bad) == 0;
+}
+
+// the full scaled Hessian G~ (lower, col-major) into w.R() for the GI fallback
+template <int P, class W>
+__device__ bool full_gram(const Prob& pb, const W& w, int l) {
+    gram_rows<P>(pb, w, w.R(), l);
+    NTM_WSYNC();
+    int bad = scale_gram<P>(w, w.R(), l);
+    NTM_WSYNC();
+    return gmaxi<P>(bad) == 0;
+}
+
+// kept for the dense-row entry point (ntm_qp_device): G~ = D G D in place,
+// F~ = D F (G given in w.R()); no state rows
+template <int P, class W>
+__device__ bool scale_phase(const W& w, int l, bool /*with_state_rows*/) {
+    const int N = w.n(), LD = w.ldj();
     if (l < N) {
         double g = w.R()[l + l * LD];
         w.D()[l] = (g > 0.0) ? 1.0 / sqrt(g) : 1.0;
@@ -391,17 +529,27 @@ __device__ bool scale_phase(const WS& w, int l, bool with_state_rows) {
         bad |= !isfinite(f);
         w.F()[l] = f;
     }
-    if (with_state_rows) {
-        for (int r = l; r < 2 * N; r += P) {
-            double s = 0.0;
-            int jmax = r >> 1;
-            for (int j = 0; j <= jmax; ++j) { double v = w.Gt()[r + j * LDG] * w.D()[j]; s += v * v; }
-            bad |= !isfinite(s) || !isfinite(w.e()[r]);
-            w.rn()[r] = s > 0.0 ? sqrt(s) : 0.0;
-        }
-    }
     NTM_WSYNC();
     return gmaxi<P>(bad) == 0;
+}
+
+// F = 2 Gamma' Om (e - R) only (NTM_MPC_Sim.m:121); G is formed on demand
+template <int P, class W>
+__device__ void f_phase(const Prob& pb, const W& w, int l) {
+    const int N = w.n();
+    const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
+    if (l < N) {
+        const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
+        double f = 0.0;
+        for (int i = l; i < N; ++i) {
+            double e0 = w.e()[2 * i] - pb.r[0], e1 = w.e()[2 * i + 1] - pb.r[1];
+            double o0 = q00 * e0 + q01 * e1;
+            double o1 = q10 * e0 + q11 * e1;
+            f += cj[2 * i] * o0 + cj[2 * i + 1] * o1;
+        }
+        w.F()[l] = 2 * f;
+    }
+    NTM_WSYNC();
 }
 
 // ---------------------------------------------------------------------------
@@ -420,6 +568,7 @@ struct Pick {
 // Implicit getWLc rows: u-bounds are -+e_j, state rows are -+Gamma_r; the
 // rows are never materialised.
 struct StructRows {
+    static constexpr bool kHasUnitRows = true;
     int N, mode;  // mode: NTM_MODE_BOX or NTM_MODE_FULL (NONE: no rows)
     double umin, umax, xmin0, xmin1, xmax0, xmax1;
 
@@ -448,31 +597,41 @@ struct StructRows {
         kind = upper ? 3 : 2;
         j = (i == 0) ? -1 : 2 * (i - 1) + c;
     }
-    __device__ double lin(const WS& w, int id, int col) const {          // Lin[id][col]
+    // u-bound row: its variable j and the sign of its GI normal (+1 lower, -1 upper); -1 otherwise
+    __device__ int unit_row(int id, int Nn, double& sg) const {
         int kind, j;
-        decode(id, w.N, kind, j);
+        decode(id, Nn, kind, j);
+        sg = (kind == 0) ? 1.0 : -1.0;
+        return kind < 2 ? j : -1;
+    }
+    template <class W>
+    __device__ double lin(const W& w, int id, int col) const {          // Lin[id][col]
+        int kind, j;
+        decode(id, w.n(), kind, j);
         if (kind < 2) return (col == j) ? (kind == 0 ? -1.0 : 1.0) : 0.0;
         if (j < 0 || col > (j >> 1)) return 0.0;
-        double g = w.Gt()[j + col * w.LDG];
+        double g = w.gt(j, col);
         return kind == 2 ? -g : g;
     }
-    __device__ double bval(const WS& w, int id) const {                  // b[id]
+    template <class W>
+    __device__ double bval(const W& w, int id) const {                  // b[id]
         int kind, j;
-        decode(id, w.N, kind, j);
+        decode(id, w.n(), kind, j);
         if (kind == 0) return -umin;
         if (kind == 1) return umax;
         int c = j & 1;
         return kind == 2 ? (-xmin(c) + w.e()[j]) : (xmax(c) - w.e()[j]);
     }
-    __device__ double rnorm(const WS& w, int id) const {
+    template <class W>
+    __device__ double rnorm(const W& w, int id) const {
         int kind, j;
-        decode(id, w.N, kind, j);
+        decode(id, w.n(), kind, j);
         return kind < 2 ? w.D()[j] : w.rn()[j];
     }
 
     // constant rows (x_0 rows; state rows with Gamma_r == 0): 0 <= b or infeasible (D15)
-    template <int P>
-    __device__ bool feasible_const(const WS& w, double x0, double x1, int l) const {
+    template <int P, class W>
+    __device__ bool feasible_const(const W& w, double x0, double x1, int l) const {
         int bad = 0;
         if (mode == NTM_MODE_FULL) {
             if (l == 0) {
@@ -481,7 +640,7 @@ struct StructRows {
                 bad |= (xmax(0) - x0) < 0.0;
                 bad |= (xmax(1) - x1) < 0.0;
             }
-            for (int r = l; r < 2 * w.N; r += P) {
+            for (int r = l; r < 2 * w.n(); r += P) {
                 if (w.rn()[r] == 0.0) {
                     int c = r & 1;
                     bad |= (w.e()[r] - xmin(c)) < 0.0;
@@ -494,9 +653,9 @@ struct StructRows {
 
     // Most violated inactive row (verify = false), or, with verify = true,
     // whether EVERY row has slack >= -tol * max(vmax, |bc|) (returned in .p).
-    template <int P>
-    __device__ Pick check(const WS& w, double Vl, int l, bool verify = false, double vmax = 1.0) const {
-        const int N = w.N;
+    template <int P, class W>
+    __device__ Pick check(const W& w, double Vl, int l, bool verify = false, double vmax = 1.0) const {
+        const int N = w.n();
         if (mode == NTM_MODE_NONE) { Pick none; none.p = verify ? 0 : -1; none.s = 0.0; none.bc = 0.0; return none; }
         double bv = kInf, bs = 0.0, bbc = 0.0;
         int bid = 0x7fffffff, bad = 0;
@@ -505,9 +664,8 @@ struct StructRows {
             if (!w.aflag()[id] && (s < bv || (s == bv && id < bid))) { bv = s; bid = id; bs = s; bbc = bcv; }
         };
         if (l < N) {
-            double Dl = w.D()[l];
-            double lo = -((-umin) / Dl);
-            double hi = umax / Dl;
+            double lo = w.vlo()[l];
+            double hi = w.vhi()[l];
             int idl = (mode == NTM_MODE_BOX) ? l : 6 * l;
             int idh = (mode == NTM_MODE_BOX) ? N + l : 6 * l + 1;
             consider(Vl - lo, idl, lo);
@@ -515,18 +673,18 @@ struct StructRows {
         }
         if (mode == NTM_MODE_FULL) {
             for (int r = l; r < 2 * N; r += P) {
-                double rnr = w.rn()[r];
-                if (rnr > 0.0) {
+                double ir = w.irn()[r];
+                if (ir > 0.0) {
                     int jmax = r >> 1;
+                    const double* gr = w.Gt() + r;           // gt(r, j) = gr[gidx(0, j)]
                     double xh = 0.0;
-                    for (int j = 0; j <= jmax; ++j) xh += w.Gt()[r + j * w.LDG] * (w.D()[j] * w.V()[j]);
-                    xh += w.e()[r];
+                    for (int j = 0; j <= jmax; ++j) xh += gr[w.gidx(0, j)] * w.U()[j];
+                    const double er = w.e()[r];
+                    xh += er;
                     int c = r & 1, i = jmax + 1;
                     int idmin = (i < N) ? 6 * i + 2 + c : 6 * N + c;
-                    double bcmin = (xmin(c) - w.e()[r]) / rnr;
-                    double bcmax = -((xmax(c) - w.e()[r]) / rnr);
-                    consider((xh - xmin(c)) / rnr, idmin, bcmin);
-                    consider((xmax(c) - xh) / rnr, idmin + 2, bcmax);
+                    consider((xh - xmin(c)) * ir, idmin, (xmin(c) - er) * ir);
+                    consider((xmax(c) - xh) * ir, idmin + 2, -((xmax(c) - er) * ir));
                 }
             }
         }
@@ -545,10 +703,10 @@ struct StructRows {
     }
 
     // GI normal n_p into w.np(); returns bc_p
-    template <int P>
-    __device__ double load_np(const WS& w, int p, int l) const {
+    template <int P, class W>
+    __device__ double load_np(const W& w, int p, int l) const {
         double rn = rnorm(w, p);
-        if (l < w.N) w.np()[l] = -((lin(w, p, l) * w.D()[l]) / rn);
+        if (l < w.n()) w.np()[l] = -((lin(w, p, l) * w.D()[l]) / rn);
         NTM_WSYNC();
         return -(bval(w, p) / rn);
     }
@@ -557,6 +715,8 @@ struct StructRows {
 // Explicit dense rows Lin U <= b (batched SoA in global memory) for the
 // quadprog-level entry point ntm_qp_device.
 struct DenseRows {
+    static constexpr bool kHasUnitRows = false;
+    __device__ int unit_row(int, int, double& sg) const { sg = 0.0; return -1; }
     const double* Lin;  // element (i, j) of scenario s at [(i + j*m)*B + s]
     const double* b;    // [i*B + s]
     double* rnrm;       // LDS, m entries
@@ -564,16 +724,19 @@ struct DenseRows {
     int m;
 
     __device__ int rows() const { return m; }
-    __device__ double lin(const WS&, int i, int j) const { return Lin[((int64_t)i + (int64_t)j * m) * B + s]; }
-    __device__ double bval(const WS&, int i) const { return b[(int64_t)i * B + s]; }
-    __device__ double rnorm(const WS&, int i) const { return rnrm[i]; }
+    template <class W>
+    __device__ double lin(const W&, int i, int j) const { return Lin[((int64_t)i + (int64_t)j * m) * B + s]; }
+    template <class W>
+    __device__ double bval(const W&, int i) const { return b[(int64_t)i * B + s]; }
+    template <class W>
+    __device__ double rnorm(const W&, int i) const { return rnrm[i]; }
 
-    template <int P>
-    __device__ int prepare_code(const WS& w, int l) {
+    template <int P, class W>
+    __device__ int prepare_code(const W& w, int l) {
         int bad = 0;
         for (int i = l; i < m; i += P) {
             double ss = 0.0;
-            for (int j = 0; j < w.N; ++j) { double v = lin(w, i, j) * w.D()[j]; ss += v * v; }
+            for (int j = 0; j < w.n(); ++j) { double v = lin(w, i, j) * w.D()[j]; ss += v * v; }
             double bi = bval(w, i);
             if (!isfinite(ss) || !isfinite(bi)) bad |= 1;
             rnrm[i] = ss > 0.0 ? sqrt(ss) : 0.0;
@@ -582,15 +745,15 @@ struct DenseRows {
         NTM_WSYNC();
         return gmaxi<P>(bad);
     }
-    template <int P>
-    __device__ Pick check(const WS& w, double Vl, int l, bool verify = false, double vmax = 1.0) const {
+    template <int P, class W>
+    __device__ Pick check(const W& w, double Vl, int l, bool verify = false, double vmax = 1.0) const {
         double bvv = kInf, bs = 0.0, bbc = 0.0;
         int bid = 0x7fffffff, bad = 0;
         for (int i = l; i < m; i += P) {
             double rn = rnrm[i];
             if (rn > 0.0 && (verify || !w.aflag()[i])) {
                 double sl = 0.0;
-                for (int j = 0; j < w.N; ++j) sl -= ((lin(w, i, j) * w.D()[j]) / rn) * w.V()[j];
+                for (int j = 0; j < w.n(); ++j) sl -= ((lin(w, i, j) * w.D()[j]) / rn) * w.V()[j];
                 double bi = bval(w, i) / rn;
                 sl += bi;
                 if (verify) bad |= sl < -1e-9 * fmax(vmax, fabs(bi));
@@ -610,10 +773,10 @@ struct DenseRows {
         pk.bc = bbc;
         return pk;
     }
-    template <int P>
-    __device__ double load_np(const WS& w, int p, int l) const {
+    template <int P, class W>
+    __device__ double load_np(const W& w, int p, int l) const {
         double rn = rnrm[p];
-        if (l < w.N) w.np()[l] = -((lin(w, p, l) * w.D()[l]) / rn);
+        if (l < w.n()) w.np()[l] = -((lin(w, p, l) * w.D()[l]) / rn);
         NTM_WSYNC();
         return -(bval(w, p) / rn);
     }
@@ -622,43 +785,48 @@ struct DenseRows {
 // ---------------------------------------------------------------------------
 // small dense kernels on a group's LDS matrices (col-major, leading dim LD)
 // ---------------------------------------------------------------------------
-// left-looking Cholesky of the n x n lower triangle of A, in place; false if not PD
+// Element (i, j) of a small matrix lives at A[i*RS + j*CS] (col-major: RS = 1,
+// CS = LD; the polish's K is stored transposed: RS = LD, CS = 1).
+// left-looking Cholesky of the n x n lower triangle of A, in place; the
+// reciprocals of the diagonal go to rdiag[0..n) (the triangular solves then
+// multiply instead of divide); false if not PD
 template <int P>
-__device__ bool chol_inplace(double* A, int n, int LD, int l) {
+__device__ bool chol_inplace(double* A, int n, int RS, int CS, int l, double* rdiag) {
     for (int k = 0; k < n; ++k) {
         double s = 0.0;
         if (l >= k && l < n) {
-            s = A[l + k * LD];
-            for (int j = 0; j < k; ++j) s -= A[l + j * LD] * A[k + j * LD];
+            s = A[l * RS + k * CS];
+            for (int j = 0; j < k; ++j) s -= A[l * RS + j * CS] * A[k * RS + j * CS];
         }
         double dk = gbcast<P>(s, k);
         if (!(dk > 0.0)) return false;
         double lk = sqrt(dk);
-        if (l > k && l < n) A[l + k * LD] = s / lk;
-        if (l == k) A[k + k * LD] = lk;
+        double il = 1.0 / lk;
+        if (l > k && l < n) A[l * RS + k * CS] = s * il;
+        if (l == k) { A[k * RS + k * CS] = lk; rdiag[k] = il; }
         NTM_WSYNC();
     }
     return true;
 }
-// lane i holds b_i in `v`; returns x_i of L x = b (L lower, col-major)
+// lane i holds b_i in `v`; returns x_i of L x = b (L lower, rdiag = 1/diag)
 template <int P>
-__device__ double fwd_lanes(const double* L, int n, int LD, double v, int l) {
+__device__ double fwd_lanes(const double* L, const double* rdiag, int n, int RS, int CS, double v, int l) {
     double acc = (l < n) ? v : 0.0, x = 0.0;
     for (int k = 0; k < n; ++k) {
-        double xk = gbcast<P>(acc, k) / L[k + k * LD];
+        double xk = gbcast<P>(acc, k) * rdiag[k];
         if (l == k) x = xk;
-        if (l > k && l < n) acc -= L[l + k * LD] * xk;
+        if (l > k && l < n) acc -= L[l * RS + k * CS] * xk;
     }
     return x;
 }
-// lane i holds b_i in `v`; returns x_i of L' x = b (L lower, col-major)
+// lane i holds b_i in `v`; returns x_i of L' x = b (L lower, rdiag = 1/diag)
 template <int P>
-__device__ double bwd_lanes(const double* L, int n, int LD, double v, int l) {
+__device__ double bwd_lanes(const double* L, const double* rdiag, int n, int RS, int CS, double v, int l) {
     double acc = (l < n) ? v : 0.0, x = 0.0;
     for (int k = n - 1; k >= 0; --k) {
-        double xk = gbcast<P>(acc, k) / L[k + k * LD];
+        double xk = gbcast<P>(acc, k) * rdiag[k];
         if (l == k) x = xk;
-        if (l < k) acc -= L[k + l * LD] * xk;
+        if (l < k) acc -= L[k * RS + l * CS] * xk;
     }
     return x;
 }
@@ -672,13 +840,14 @@ __device__ double bwd_lanes(const double* L, int n, int LD, double v, int l) {
 // reduction instead of a Givens chain); drops restore R with a Givens sweep
 // (Goldfarb & Idnani 1983, section 3).
 // ---------------------------------------------------------------------------
-template <int P, class Rows>
-__device__ int gi_solve(const WS& w, const Rows* rows, int nrows, int l, int* iters_out, int* q_out) {
-    const int N = w.N, LD = w.LDJ, LDJ = w.LDJ;
+template <int P, class Rows, class W>
+__device__ int gi_solve(const W& w, const Rows* rows, int nrows, int l, int* iters_out, int* q_out) {
+    const int N = w.n(), LD = w.ldj(), LDJ = w.ldj();
     *iters_out = 0;
     *q_out = 0;
+    NTM_T0(tg);
     // 1. Cholesky G~ = L L' (in place in w.R())
-    if (!chol_inplace<P>(w.R(), N, LD, l)) return NTM_EXIT_NONFINITE;
+    if (!chol_inplace<P>(w.R(), N, 1, LD, l, w.ldi())) return NTM_EXIT_NONFINITE;
     // 2. J = L^{-T}: lane c computes row c of J (= column c of L^{-1})
     if (l < N) {
         for (int i = 0; i < N; ++i) {
@@ -686,7 +855,7 @@ __device__ int gi_solve(const WS& w, const Rows* rows, int nrows, int l, int* it
             if (i >= l) {
                 x = (i == l) ? 1.0 : 0.0;
                 for (int k2 = l; k2 < i; ++k2) x -= w.R()[i + k2 * LD] * w.J()[l * LDJ + k2];
-                x /= w.R()[i + i * LD];
+                x *= w.ldi()[i];
             }
             w.J()[l * LDJ + i] = x;
         }
@@ -704,28 +873,43 @@ __device__ int gi_solve(const WS& w, const Rows* rows, int nrows, int l, int* it
             for (int k2 = 0; k2 < N; ++k2) v += w.J()[l * LDJ + k2] * w.d()[k2];
             Vl = -v;
             w.V()[l] = Vl;
+            w.U()[l] = w.D()[l] * Vl;
         }
         NTM_WSYNC();
     }
+    NTM_ACC(ST_GI_FACT, tg);
     if (!rows) return NTM_EXIT_OPTIMAL;
     const int max_iter = 10 * (N + nrows) + 50;
     int q = 0, it = 0;
     for (;;) {
         Pick pk = rows->template check<P>(w, Vl, l);
         double vmax = gmax<P>(l < N ? fabs(Vl) : 0.0);
+        NTM_ACC(ST_GI_CHECK, tg);
+        NTM_CNT(CN_CHECK);
         if (pk.p < 0 || pk.s >= -1e-12 * fmax(fmax(1.0, vmax), fabs(pk.bc))) {
             *iters_out = it;
             *q_out = q;
             return NTM_EXIT_OPTIMAL;
         }
         const int p = pk.p;
-        const double bcp = rows->template load_np<P>(w, p, l);
+        const double bcp = uni<P>(rows->template load_np<P>(w, p, l));
+        // u-bound rows have n_p = -+e_j: d = J' n_p is then a signed row of J
+        int ej = -1;
+        double esg = 0.0;
+        if constexpr (Rows::kHasUnitRows) {
+            ej = uni<P>(rows->unit_row(p, N, esg));
+            esg = uni<P>(esg);
+        }
         double upq = 0.0;   // multiplier of the constraint being added
         for (;;) {
             if (++it > max_iter) { *iters_out = it; *q_out = q; return NTM_EXIT_MAXITER; }
             // d = J' n_p
             double dl = 0.0;
-            if (l < N) for (int i = 0; i < N; ++i) dl += w.J()[i * LDJ + l] * w.np()[i];
+            if (ej >= 0) {
+                if (l < N) dl = esg * w.J()[ej * LDJ + l];
+            } else if (l < N) {
+                for (int i = 0; i < N; ++i) dl += w.J()[i * LDJ + l] * w.np()[i];
+            }
             if (l < N) w.d()[l] = dl;
             NTM_WSYNC();
             // z = J2 d2 (primal direction)
@@ -734,7 +918,7 @@ __device__ int gi_solve(const WS& w, const Rows* rows, int nrows, int l, int* it
             // r = R^{-1} d1 (negative dual direction), back substitution
             double acc = (l < q) ? dl : 0.0, rl = 0.0;
             for (int b = q - 1; b >= 0; --b) {
-                double rb = gbcast<P>(acc, b) / w.R()[b + b * LD];
+                double rb = gbcast<P>(acc, b) * w.rinv()[b];
                 if (l == b) rl = rb;
                 if (l < b) acc -= w.R()[l + b * LD] * rb;
             }
@@ -750,14 +934,15 @@ __device__ int gi_solve(const WS& w, const Rows* rows, int nrows, int l, int* it
             double zn = gsum<P>((l >= q && l < N) ? dl * dl : 0.0);
             double sp = gsum<P>(npl * Vl) - bcp;
             double dnrm = gsum<P>(dl * dl);
-            double t2 = (zn <= 1e-300 || sqrt(zn) <= kDepTol * sqrt(dnrm)) ? kInf : -sp / zn;
+            double t2 = (zn <= 1e-300 || zn <= (kDepTol * kDepTol) * dnrm) ? kInf : -sp / zn;
             double t = fmin(t1, t2);
+            NTM_ACC(ST_GI_DIR, tg);
             if (!(t < kInf)) { *iters_out = it; *q_out = q; return NTM_EXIT_INFEASIBLE; }
             if (l < q) w.uu()[l] = fmax(0.0, w.uu()[l] - t * rl);
             upq += t;
             if (t2 < kInf) {
                 Vl += t * zl;
-                if (l < N) w.V()[l] = Vl;
+                if (l < N) { w.V()[l] = Vl; w.U()[l] = w.D()[l] * Vl; }
                 if (t == t2) {
                     // ---- add p: Householder on d[q:N] -> J(:, q:N) ----
                     double dq2 = (l >= q && l < N) ? dl * dl : 0.0;
@@ -780,18 +965,20 @@ __device__ int gi_solve(const WS& w, const Rows* rows, int nrows, int l, int* it
                     if (l < q) w.R()[l + q * LD] = dl;
                     if (l == q) {
                         w.R()[q + q * LD] = h;
+                        w.rinv()[q] = 1.0 / h;
                         w.act()[q] = p;
                         w.aflag()[p] = 1;
                         w.uu()[q] = upq;
                     }
                     ++q;
                     NTM_WSYNC();
+                    NTM_ACC(ST_GI_ADD, tg);
                     break;
                 }
             }
             // ---- drop active position li (partial or dual-only step) ----
             const int l0 = li;
-            const int dropped = w.act()[l0];
+            const int dropped = uni<P>(w.act()[l0]);
             NTM_WSYNC();
             if (l < q) {
                 for (int c = l0; c < q - 1; ++c) w.R()[l + c * LD] = w.R()[l + (c + 1) * LD];
@@ -807,15 +994,17 @@ __device__ int gi_solve(const WS& w, const Rows* rows, int nrows, int l, int* it
             }
             NTM_WSYNC();
             for (int j = l0; j < q - 1; ++j) {
-                double a = w.R()[j + j * LD], bq = w.R()[(j + 1) + j * LD];
+                double a = uni<P>(w.R()[j + j * LD]), bq = uni<P>(w.R()[(j + 1) + j * LD]);
                 double hh = hypot(a, bq);
                 double cc = 1.0, ss = 0.0;
                 if (hh != 0.0) { cc = a / hh; ss = bq / hh; }
                 NTM_WSYNC();
                 if (l >= j && l < q - 1) {
                     double r1 = w.R()[j + l * LD], r2 = w.R()[(j + 1) + l * LD];
-                    w.R()[j + l * LD] = cc * r1 + ss * r2;
+                    double nr = cc * r1 + ss * r2;
+                    w.R()[j + l * LD] = nr;
                     w.R()[(j + 1) + l * LD] = (l == j) ? 0.0 : (-ss * r1 + cc * r2);
+                    if (l == j) w.rinv()[j] = 1.0 / nr;
                 }
                 if (l < N) {
                     double j1 = w.J()[l * LDJ + j], j2 = w.J()[l * LDJ + j + 1];
@@ -825,6 +1014,7 @@ __device__ int gi_solve(const WS& w, const Rows* rows, int nrows, int l, int* it
                 NTM_WSYNC();
             }
             --q;
+            NTM_ACC(ST_GI_DROP, tg);
         }
     }
 }
@@ -839,10 +1029,10 @@ __device__ int gi_solve(const WS& w, const Rows* rows, int nrows, int l, int* it
 //   Writes w.U() (unscaled U).  G~ comes from Gamma (gram, structured rows) or
 //   from Gsave (a copy taken before the GI factorisation, dense rows).
 // ---------------------------------------------------------------------------
-template <int P, class Rows>
-__device__ bool polish_phase(const Prob& pb, const WS& w, const Rows* rows, int q, int l,
+template <int P, class Rows, class W>
+__device__ bool polish_phase(const Prob& pb, const W& w, const Rows* rows, int q, int l,
                              const double* Gsave, bool g_in_R, bool verify_only, int* ns_out) {
-    const int N = w.N, LD = w.LDJ, LDJ = w.LDJ;
+    const int N = w.n(), LD = w.ldj(), LDJ = w.ldj();
     const double Vgi = (l < N) ? w.V()[l] : 0.0;
     // --- classify active rows ---
     if (l < N) w.fx()[l] = 0;
@@ -896,10 +1086,10 @@ __device__ bool polish_phase(const Prob& pb, const WS& w, const Rows* rows, int 
             if (fixed || w.fx()[j]) w.R()[l + j * LD] = (j == l) ? 1.0 : 0.0;
     }
     NTM_WSYNC();
-    bool ok = chol_inplace<P>(w.R(), N, LD, l);
+    bool ok = chol_inplace<P>(w.R(), N, 1, LD, l, w.ldi());
     double vfin = 0.0;
     if (ok) {
-        double wl = fwd_lanes<P>(w.R(), N, LD, gl, l);      // w = L^{-1} g
+        double wl = fwd_lanes<P>(w.R(), w.ldi(), N, 1, LD, gl, l);      // w = L^{-1} g
         double tl = -wl;
         if (nS > 0) {
             // E' into Y (= w.J(), row-major N x nS), h_s
@@ -925,26 +1115,27 @@ __device__ bool polish_phase(const Prob& pb, const WS& w, const Rows* rows, int 
                 for (int i = 0; i < N; ++i) {
                     double y = w.J()[i * LDJ + l];
                     for (int k = 0; k < i; ++k) y -= w.R()[i + k * LD] * w.J()[k * LDJ + l];
-                    w.J()[i * LDJ + l] = y / w.R()[i + i * LD];
+                    w.J()[i * LDJ + l] = y * w.ldi()[i];
                 }
             }
             NTM_WSYNC();
-            // K = Y'Y (lower, col-major in w.M()); rhs = h + Y'w
+            // K = Y'Y (lower triangle stored transposed in R's strict upper part); rhs = h + Y'w
+            double* K = w.R() + LD;
             double rhs = 0.0;
             if (l < nS) {
                 for (int c = 0; c <= l; ++c) {
                     double sK = 0.0;
                     for (int i = 0; i < N; ++i) sK += w.J()[i * LDJ + l] * w.J()[i * LDJ + c];
-                    w.M()[l + c * LD] = sK;
+                    K[l * LD + c] = sK;
                 }
                 rhs = hs;
                 for (int i = 0; i < N; ++i) rhs += w.J()[i * LDJ + l] * w.d()[i];
             }
             NTM_WSYNC();
-            ok = chol_inplace<P>(w.M(), nS, LD, l);
+            ok = chol_inplace<P>(K, nS, LD, 1, l, w.kdi());
             if (ok) {
-                double t1 = fwd_lanes<P>(w.M(), nS, LD, rhs, l);
-                double mu = bwd_lanes<P>(w.M(), nS, LD, t1, l);
+                double t1 = fwd_lanes<P>(K, w.kdi(), nS, LD, 1, rhs, l);
+                double mu = bwd_lanes<P>(K, w.kdi(), nS, LD, 1, t1, l);
                 if (l < nS) w.np()[l] = mu;
                 NTM_WSYNC();
                 if (l < N) {
@@ -955,7 +1146,7 @@ __device__ bool polish_phase(const Prob& pb, const WS& w, const Rows* rows, int 
             }
         }
         if (ok) {
-            double vl = bwd_lanes<P>(w.R(), N, LD, tl, l);  // V_F = L^{-T} t
+            double vl = bwd_lanes<P>(w.R(), w.ldi(), N, 1, LD, tl, l);  // V_F = L^{-T} t
             vfin = fixed ? vb : vl;
         }
     }
@@ -979,7 +1170,7 @@ __device__ bool polish_phase(const Prob& pb, const WS& w, const Rows* rows, int 
             // through Gamma: y = Gamma (D V), grad_j = D_j 2 Gamma_j' Om y + F~_j
             for (int r = l; r < 2 * N; r += P) {
                 double y = 0.0;
-                for (int j = 0; j <= (r >> 1); ++j) y += w.Gt()[r + j * w.LDG] * (w.D()[j] * w.V()[j]);
+                for (int j = 0; j <= (r >> 1); ++j) y += w.gt(r, j) * (w.D()[j] * w.V()[j]);
                 w.xp()[r] = y;              // scratch: xp is rewritten by the rollout
             }
             NTM_WSYNC();
@@ -988,7 +1179,7 @@ __device__ bool polish_phase(const Prob& pb, const WS& w, const Rows* rows, int 
                 for (int i = l; i < N; ++i) {
                     double y0 = w.xp()[2 * i], y1 = w.xp()[2 * i + 1];
                     double o0 = pb.Q[0] * y0 + pb.Q[1] * y1, o1 = pb.Q[2] * y0 + pb.Q[3] * y1;
-                    g2 += w.Gt()[2 * i + l * w.LDG] * o0 + w.Gt()[2 * i + 1 + l * w.LDG] * o1;
+                    g2 += w.gt(2 * i, l) * o0 + w.gt(2 * i + 1, l) * o1;
                 }
                 res = w.D()[l] * (2 * g2) + w.F()[l];
             }
@@ -1029,12 +1220,241 @@ __device__ bool polish_phase(const Prob& pb, const WS& w, const Rows* rows, int 
 }
 
 // ---------------------------------------------------------------------------
+// Exact re-solve on an active set, compact form for the implicit getWLc rows
+// (oracle: polish_active_set).  Used both to VERIFY a warm-start candidate
+// (the active set of LPV iteration it-2) and to POLISH the Goldfarb-Idnani
+// result.  Single-entry rows fix their variable exactly (U_j = b/Lin_j); the
+// nF free variables and the nS general (state) rows form a small KKT system
+//   min 1/2 V_F' G~_FF V_F + g_F' V_F  s.t. E V_F = h
+// solved in compact nF / nS coordinates: G~_FF from Gamma's free columns
+// (bit-identical entries to the full Gram), g_F = D_F 2 Gamma_F' Om (Gamma U_B
+// + e - r) by two O(N) passes, Cholesky of G~_FF, Schur complement
+// K = E G~_FF^{-1} E'.  Accepted only if the KKT certificate holds (primal
+// slack on every row, multiplier signs).  Writes w.U()/w.V() on success or
+// when !verify_only (then GI's V is kept); returns success.
+// ---------------------------------------------------------------------------
+template <int P, class W>
+__device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* rows, int q, int l, bool verify_only,
+                               int* ns_out) {
+    const int N = w.n(), LD = w.ldj(), LDJ = w.ldj();
+    const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
+    const double Vprev = (l < N) ? w.V()[l] : 0.0;
+    // --- classify active rows: single-entry rows fix a variable, the rest are general ---
+    if (l < N) w.fx()[l] = 0;
+    NTM_WSYNC();
+    int isgen = 0, fixj = -1, id = -1, srow = 0;
+    double ufix = 0.0, nfix = 0.0, ssign = 0.0;
+    if (l < q) {
+        id = w.act()[l];
+        int kind, j;
+        rows->decode(id, N, kind, j);
+        if (kind < 2) {                                   // u bound: Lin = -+e_j, b = -umin / umax
+            fixj = j;
+            double lv = kind == 0 ? -1.0 : 1.0;
+            ufix = rows->bval(w, id) / lv;
+            nfix = -((lv * w.D()[j]) / w.D()[j]);
+        } else {                                          // state row r = j: Lin = -+Gamma_r
+            const double sg = (kind == 2) ? -1.0 : 1.0;
+            int nnz = 0, jj = -1;
+            for (int c = 0; c <= (j >> 1); ++c) if (w.gt(j, c) != 0.0) { ++nnz; jj = c; }
+            if (nnz == 1) {
+                double lv = sg * w.gt(j, jj);
+                fixj = jj;
+                ufix = rows->bval(w, id) / lv;
+                nfix = -((lv * w.D()[jj]) / w.rn()[j]);
+            } else {
+                isgen = 1;
+                srow = j;
+                ssign = sg;
+            }
+        }
+    }
+    const int lane = threadIdx.x & 63;
+    const unsigned long long gmask = (P == 64) ? ~0ull : (((1ull << P) - 1ull) << (lane & ~(P - 1)));
+    const unsigned long long below = (1ull << lane) - 1ull;
+    unsigned long long bal = __ballot(isgen) & gmask;
+    const int nS = uni<P>((int)__popcll(bal));
+    if (ns_out) *ns_out = nS;
+    if (l < q) {
+        if (isgen) {
+            const int k = __popcll(bal & below);
+            w.sidx()[k] = id;
+            w.srw()[k] = srow;
+            w.ssg()[k] = ssign;
+        } else {
+            w.fx()[fixj] = 1;
+            w.Uf()[fixj] = ufix;
+            w.hv()[fixj] = nfix;
+        }
+    }
+    NTM_WSYNC();
+    const bool fixed = (l < N) && w.fx()[l];
+    const double uf = fixed ? w.Uf()[l] : 0.0;
+    const double vb = fixed ? uf / w.D()[l] : 0.0;
+    if (l < N) w.Vb()[l] = vb;
+    // --- compact map of the free variables ---
+    bal = __ballot((l < N) && !fixed) & gmask;
+    const int nF = uni<P>((int)__popcll(bal));
+    const int fpos = __popcll(bal & below);
+    if (l < N && !fixed) w.fidx()[fpos] = l;
+    // --- z = Gamma U_B + e - r (scratch in w.xp(), rewritten by the rollout) ---
+    for (int r = l; r < 2 * N; r += P) {
+        double y = 0.0;
+        for (int j = 0; j <= (r >> 1); ++j)
+            if (w.fx()[j]) y += w.gt(r, j) * w.Uf()[j];
+        w.xp()[r] = y + w.e()[r] - pb.r[r & 1];
+    }
+    NTM_WSYNC();
+    // --- g_F (lane k = compact index) and the compact G~_FF (lower, col-major in R) ---
+    double gl = 0.0;
+    if (l < nF) {
+        const int ja = w.fidx()[l];
+        const double* ca = w.Gt() + w.gidx(2 * ja, ja) - 2 * ja;
+        double g2 = 0.0;
+        for (int i = ja; i < N; ++i) {
+            double z0 = w.xp()[2 * i], z1 = w.xp()[2 * i + 1];
+            g2 += ca[2 * i] * (q00 * z0 + q01 * z1) + ca[2 * i + 1] * (q10 * z0 + q11 * z1);
+        }
+        gl = w.D()[ja] * (2 * g2);
+        for (int c = 0; c <= l; ++c) {
+            const int jc = w.fidx()[c];
+            const double* cc = w.Gt() + w.gidx(2 * jc, jc) - 2 * jc;
+            double sg = 0.0;
+            for (int i = ja; i < N; ++i) {
+                double g0 = cc[2 * i], g1 = cc[2 * i + 1];
+                double o0 = q00 * g0 + q01 * g1;
+                double o1 = q10 * g0 + q11 * g1;
+                sg += ca[2 * i] * o0;
+                sg += ca[2 * i + 1] * o1;
+            }
+            w.R()[l + c * LD] = (2 * sg) * w.D()[ja] * w.D()[jc];
+        }
+    }
+    NTM_WSYNC();
+    // GI normal of general row s at variable j: n = -(Lin_j D_j)/rn, Lin = sg Gamma_r
+    auto gen_n = [&](int s2, int j) -> double {
+        const int r = w.srw()[s2];
+        return (j <= (r >> 1)) ? -(((w.ssg()[s2] * w.gt(r, j)) * w.D()[j]) * w.irn()[r]) : 0.0;
+    };
+    bool ok = chol_inplace<P>(w.R(), nF, 1, LD, l, w.ldi());
+    double vfin = 0.0;
+    if (ok) {
+        const double wl = fwd_lanes<P>(w.R(), w.ldi(), nF, 1, LD, gl, l);    // L^{-1} g_F
+        double tl = -wl;
+        if (nS > 0) {
+            // E' (compact rows) into Y = w.J() (row-major nF x nS) and h
+            if (l < nF) {
+                const int j = w.fidx()[l];
+                for (int s2 = 0; s2 < nS; ++s2) w.J()[l * LDJ + s2] = gen_n(s2, j);
+                w.d()[l] = wl;
+            }
+            double hs = 0.0;
+            if (l < nS) {
+                const int r = w.srw()[l];
+                const int c = r & 1;
+                const double bval = (w.ssg()[l] > 0.0) ? (rows->xmax(c) - w.e()[r]) : (-rows->xmin(c) + w.e()[r]);
+                hs = -(bval * w.irn()[r]);
+                for (int j = 0; j <= (r >> 1); ++j)
+                    if (w.fx()[j]) hs -= gen_n(l, j) * w.Vb()[j];
+            }
+            NTM_WSYNC();
+            if (l < nS) {                          // Y = L^{-1} E': lane s solves column s
+                for (int i = 0; i < nF; ++i) {
+                    double y = w.J()[i * LDJ + l];
+                    for (int k = 0; k < i; ++k) y -= w.R()[i + k * LD] * w.J()[k * LDJ + l];
+                    w.J()[i * LDJ + l] = y * w.ldi()[i];
+                }
+            }
+            NTM_WSYNC();
+            double* K = w.R() + LD;                // K(a, c), a >= c, at R[c + (a+1) LD]
+            double rhs = 0.0;
+            if (l < nS) {
+                for (int c = 0; c <= l; ++c) {
+                    double sK = 0.0;
+                    for (int i = 0; i < nF; ++i) sK += w.J()[i * LDJ + l] * w.J()[i * LDJ + c];
+                    K[l * LD + c] = sK;
+                }
+                rhs = hs;
+                for (int i = 0; i < nF; ++i) rhs += w.J()[i * LDJ + l] * w.d()[i];
+            }
+            NTM_WSYNC();
+            ok = chol_inplace<P>(K, nS, LD, 1, l, w.kdi());
+            if (ok) {
+                double t1 = fwd_lanes<P>(K, w.kdi(), nS, LD, 1, rhs, l);
+                double mu = bwd_lanes<P>(K, w.kdi(), nS, LD, 1, t1, l);
+                if (l < nS) w.np()[l] = mu;
+                NTM_WSYNC();
+                if (l < nF) {
+                    double sY = 0.0;
+                    for (int a = 0; a < nS; ++a) sY += w.J()[l * LDJ + a] * w.np()[a];
+                    tl = sY - wl;
+                }
+            }
+        }
+        if (ok) {
+            const double vF = bwd_lanes<P>(w.R(), w.ldi(), nF, 1, LD, tl, l);   // compact V_F
+            const double vsc = __shfl(vF, (l < N && !fixed) ? fpos : 0, P);
+            vfin = fixed ? vb : vsc;
+        }
+    }
+    if (ok) {
+        // ---- KKT certificate ----
+        if (l < N) { w.V()[l] = vfin; w.U()[l] = w.D()[l] * vfin; }
+        NTM_WSYNC();
+        double vmax = gmax<P>(l < N ? fabs(vfin) : 0.0);
+        Pick vf = rows->template check<P>(w, vfin, l, true, fmax(1.0, vmax));
+        ok = vf.p == 0;
+        // gradient G~V + F~ = D (2 Gamma' Om (Gamma D V) ) + F~ through Gamma
+        for (int r = l; r < 2 * N; r += P) {
+            double y = 0.0;
+            for (int j = 0; j <= (r >> 1); ++j) y += w.gt(r, j) * w.U()[j];
+            w.xp()[r] = y;
+        }
+        NTM_WSYNC();
+        double res = 0.0;
+        if (l < N) {
+            const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;
+            double g2 = 0.0;
+            for (int i = l; i < N; ++i) {
+                double y0 = w.xp()[2 * i], y1 = w.xp()[2 * i + 1];
+                g2 += cl[2 * i] * (q00 * y0 + q01 * y1) + cl[2 * i + 1] * (q10 * y0 + q11 * y1);
+            }
+            res = w.D()[l] * (2 * g2) + w.F()[l];
+            for (int s2 = 0; s2 < nS; ++s2) res -= w.np()[s2] * gen_n(s2, l);
+        }
+        double mval = 0.0;
+        bool has = false;
+        if (l < nS) { mval = w.np()[l]; has = true; }
+        if (fixed) {
+            double lam = res / w.hv()[l];
+            mval = has ? fmin(mval, lam) : lam;
+            has = true;
+        }
+        double mabs = gmax<P>(has ? fabs(mval) : 0.0);
+        double mmin = -gmax<P>(has ? -mval : -kInf);
+        ok = ok && !(mmin < -1e-9 * fmax(1.0, mabs));
+    }
+    ok = gmaxi<P>(ok ? 0 : 1) == 0;
+    if (verify_only && !ok) {
+        if (l < N) w.V()[l] = Vprev;
+        NTM_WSYNC();
+        return false;
+    }
+    if (l < N) {
+        w.U()[l] = ok ? (fixed ? uf : vfin * w.D()[l]) : Vprev * w.D()[l];
+        w.V()[l] = ok ? vfin : Vprev;
+    }
+    NTM_WSYNC();
+    return ok;
+}
+
+// ---------------------------------------------------------------------------
 // rollout + scheduling update + convergence (NTM_MPC_Sim.m:110-117, 123-127)
 // Returns (group-uniform) whether sum|Uold - U| < eps; updates Uold.
 // ---------------------------------------------------------------------------
-template <int P>
-__device__ bool rollout_phase(const Prob& pb, const WS& w, double x0, double x1, int l) {
-    const int N = w.N;
+template <int P, class W>
+__device__ bool rollout_phase(const Prob& pb, const W& w, double x0, double x1, int l) {
+    const int N = w.n();
     const Coef& k = pb.k;
     if (l == 0) {
         double y0 = x0, y1 = x1;
@@ -1081,19 +1501,22 @@ __device__ __forceinline__ void plant_step(const Prob& pb, double x0, double x1,
 // ---------------------------------------------------------------------------
 // one inner iteration's QP: build -> scale -> GI -> polish -> w.U()
 // ---------------------------------------------------------------------------
-template <int P>
-__device__ int qp_phase(const Prob& pb, const WS& w, double x0, double x1, int l, int* qp_iters,
+template <int P, class W>
+__device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l, int* qp_iters,
                         int* q_out, int* ns_out, int slot) {
-    const int N = w.N;
+    const int N = w.n();
+    NTM_T0(tq);
     lift_phase<P>(pb, w, l);
+    NTM_ACC(ST_LIFT, tq);
     free_response<P>(w, x0, x1, l);
-    cost_phase<P>(pb, w, l);
+    f_phase<P>(pb, w, l);
+    NTM_ACC(ST_COST, tq);
     const bool full = pb.mode == NTM_MODE_FULL;
     int flag, q = 0, ns = 0;
     *qp_iters = 0;
     StructRows rows(pb);
     int* cand = w.cand() + slot * (N + 1);
-    if (!scale_phase<P>(w, l, full)) {
+    if (!diag_scale_phase<P>(pb, w, l, full)) {
         flag = NTM_EXIT_NONFINITE;
     } else {
         const int nrows = (pb.mode == NTM_MODE_NONE) ? 0 : rows.rows();
@@ -1104,31 +1527,36 @@ __device__ int qp_phase(const Prob& pb, const WS& w, double x0, double x1, int l
         if (pb.mode != NTM_MODE_NONE && !rows.template feasible_const<P>(w, x0, x1, l)) {
             flag = NTM_EXIT_INFEASIBLE;
         } else {
+            NTM_ACC(ST_SCALE, tq);
             bool done = false;
             // warm start: the LPV loop alternates between two QPs (a 2-cycle),
             // so the active set of iteration it-2 is tried first; it is taken
             // only if the exact active-set solve passes the KKT certificate
             // (the optimum of this strictly convex QP is unique).
-            const int cq = cand[N];
+            const int cq = uni<P>(cand[N]);
             if (cq >= 0) {
+                NTM_CNT(CN_CAND);
                 if (l < cq) w.act()[l] = cand[l];
                 NTM_WSYNC();
-                if (polish_phase<P, StructRows>(pb, w, &rows, cq, l, nullptr, true, true, &ns)) {
+                if (polish_compact<P>(pb, w, &rows, cq, l, true, &ns)) {
                     flag = NTM_EXIT_OPTIMAL;
                     q = cq;
                     done = true;
-                } else {
-                    gram_rows<P>(pb, w, w.R(), l);    // the verification factored w.R()
-                    NTM_WSYNC();
-                    (void)scale_gram<P>(w, w.R(), l);
-                    NTM_WSYNC();
+                    NTM_CNT(CN_HIT);
                 }
+                NTM_ACC(ST_CAND, tq);
             }
             if (!done) {
-                flag = gi_solve<P, StructRows>(w, pb.mode == NTM_MODE_NONE ? nullptr : &rows, nrows, l,
-                                               qp_iters, &q);
-                if (flag == NTM_EXIT_OPTIMAL)
-                    (void)polish_phase<P, StructRows>(pb, w, &rows, q, l, nullptr, false, false, &ns);
+                if (!full_gram<P>(pb, w, l)) {
+                    flag = NTM_EXIT_NONFINITE;
+                } else {
+                    NTM_ACC(ST_REGRAM, tq);
+                    flag = gi_solve<P, StructRows, W>(w, pb.mode == NTM_MODE_NONE ? nullptr : &rows, nrows, l,
+                                                      qp_iters, &q);
+                    NTM_ACC(ST_GI, tq);
+                    if (flag == NTM_EXIT_OPTIMAL) (void)polish_compact<P>(pb, w, &rows, q, l, false, &ns);
+                    NTM_ACC(ST_POLISH, tq);
+                }
             }
         }
     }

@@ -14,6 +14,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -21,20 +22,24 @@
 
 using namespace ntm;
 
+#ifdef NTM_STAMPS
+__device__ unsigned long long ntm::ntm_stamps[16];
+#endif
+
 namespace {
 
-template <int P>
-__device__ __forceinline__ void load_state(const WS& w, int64_t B, int64_t s, const double* rho,
+template <int P, class W>
+__device__ __forceinline__ void load_state(const W& w, int64_t B, int64_t s, const double* rho,
                                            const double* U_old, int l) {
-    const int N = w.N;
+    const int N = w.n();
     for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[(int64_t)e * B + s];
     if (l < N) w.Uold()[l] = U_old[(int64_t)l * B + s];
     NTM_WSYNC();
 }
 
 // one MPC step on LDS-resident state; returns exit flag, sets *iters
-template <int P>
-__device__ int mpc_step_dev(const Prob& pb, const WS& w, double x0, double x1, int l, int* iters,
+template <int P, class W>
+__device__ int mpc_step_dev(const Prob& pb, const W& w, double x0, double x1, int l, int* iters,
                             int64_t B = 0, int64_t s = 0) {
     int flag = NTM_EXIT_OPTIMAL, it;
     int n_qp = 0, n_gi = 0, n_act = 0, n_gen = 0;
@@ -45,7 +50,10 @@ __device__ int mpc_step_dev(const Prob& pb, const WS& w, double x0, double x1, i
         n_gi += qi;
         n_act += qa;
         n_gen += ns;
-        if (rollout_phase<P>(pb, w, x0, x1, l)) break;
+        NTM_T0(tr);
+        bool conv = rollout_phase<P>(pb, w, x0, x1, l);
+        NTM_ACC(ST_ROLL, tr);
+        if (conv) break;
     }
     *iters = it > pb.i_sim ? pb.i_sim : it;
     if (pb.stats && l == 0) {
@@ -57,8 +65,11 @@ __device__ int mpc_step_dev(const Prob& pb, const WS& w, double x0, double x1, i
     return flag;
 }
 
-template <int P>
-__global__ __launch_bounds__(64) void k_mpc_step(Prob pb, int64_t B, const double* __restrict__ x_k,
+#ifndef NTM_HOT_WAVES_PER_EU
+#define NTM_HOT_WAVES_PER_EU 2
+#endif
+template <int P, int NN>
+__global__ __launch_bounds__(64, NTM_HOT_WAVES_PER_EU) void k_mpc_step(Prob pb, int64_t B, const double* __restrict__ x_k,
                                                  double* __restrict__ rho, double* __restrict__ U_old,
                                                  double* __restrict__ U, double* __restrict__ x_pred,
                                                  double* __restrict__ x_next, int32_t* __restrict__ exitflag,
@@ -67,9 +78,10 @@ __global__ __launch_bounds__(64) void k_mpc_step(Prob pb, int64_t B, const doubl
     constexpr int G = 64 / P;
     const int g = threadIdx.x / P, l = threadIdx.x % P;
     const int64_t s = (int64_t)blockIdx.x * G + g;
-    const int N = pb.N;
+    const int N = NN > 0 ? NN : pb.N;
+    NTM_STAMPS_INIT();
     if (s >= B) return;
-    WS w = ws_carve(smem + g * ws_bytes(N), N);
+    auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
     const double x0 = x_k[s], x1 = x_k[B + s];
     if (l < 2) w.cand()[l * (N + 1) + N] = -1;
     load_state<P>(w, B, s, rho, U_old, l);
@@ -89,19 +101,20 @@ __global__ __launch_bounds__(64) void k_mpc_step(Prob pb, int64_t B, const doubl
         exitflag[s] = flag;
         inner_iters[s] = its;
     }
+    NTM_STAMPS_FLUSH();
 }
 
-template <int P>
-__global__ __launch_bounds__(64) void k_mpc_run(Prob pb, int64_t B, int k_sim, const double* __restrict__ x0v,
+template <int P, int NN>
+__global__ __launch_bounds__(64, NTM_HOT_WAVES_PER_EU) void k_mpc_run(Prob pb, int64_t B, int k_sim, const double* __restrict__ x0v,
                                                 double* xk, double* uk, double* Uk, double* wpred,
                                                 int32_t* exitflag, int32_t* inner_iters) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int G = 64 / P;
     const int g = threadIdx.x / P, l = threadIdx.x % P;
     const int64_t s = (int64_t)blockIdx.x * G + g;
-    const int N = pb.N;
+    const int N = NN > 0 ? NN : pb.N;
     if (s >= B) return;
-    WS w = ws_carve(smem + g * ws_bytes(N), N);
+    auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
     double x0 = x0v[s], x1 = x0v[B + s];
     if (l < 2) w.cand()[l * (N + 1) + N] = -1;
     {   // Rho = repmat(rho(x0), 1, N) (NTM_MPC_Sim.m:63-65); Uold = +inf (D14)
@@ -158,7 +171,7 @@ __global__ void k_AB(Prob pb, int64_t B, const double* rho, double* A, double* B
     Bv[B + s] = 0.0;
 }
 
-template <int P>
+template <int P, int NN>
 __global__ __launch_bounds__(64) void k_lift(Prob pb, int64_t B, const double* rho, double* Phi, double* Gam,
                                              double* Lam) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -167,7 +180,7 @@ __global__ __launch_bounds__(64) void k_lift(Prob pb, int64_t B, const double* r
     const int64_t s = (int64_t)blockIdx.x * G + g;
     const int N = pb.N, R = 2 * N;
     if (s >= B) return;
-    WS w = ws_carve(smem + g * ws_bytes(N), N);
+    auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
     for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[(int64_t)e * B + s];
     NTM_WSYNC();
     lift_phase<P>(pb, w, l);
@@ -180,19 +193,22 @@ __global__ __launch_bounds__(64) void k_lift(Prob pb, int64_t B, const double* r
         Lam[(int64_t)(2 * i) * B + s] = w.Lam()[2 * i];
         Lam[(int64_t)(2 * i + 1) * B + s] = w.Lam()[2 * i + 1];
     }
-    for (int e = l; e < R * N; e += P) Gam[(int64_t)e * B + s] = w.Gt()[e];
+    for (int e = l; e < R * N; e += P) {
+        int r = e % R, j = e / R;
+        Gam[(int64_t)e * B + s] = (r >= 2 * j) ? w.gt(r, j) : 0.0;
+    }
 }
 
-template <int P>
+template <int P, int NN>
 __global__ __launch_bounds__(64) void k_cost(Prob pb, int64_t B, const double* rho, const double* x,
                                              double* G_out, double* F_out) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int G = 64 / P;
     const int g = threadIdx.x / P, l = threadIdx.x % P;
     const int64_t s = (int64_t)blockIdx.x * G + g;
-    const int N = pb.N;
+    const int N = NN > 0 ? NN : pb.N;
     if (s >= B) return;
-    WS w = ws_carve(smem + g * ws_bytes(N), N);
+    auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
     for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[(int64_t)e * B + s];
     NTM_WSYNC();
     lift_phase<P>(pb, w, l);
@@ -200,7 +216,7 @@ __global__ __launch_bounds__(64) void k_cost(Prob pb, int64_t B, const double* r
     cost_phase<P>(pb, w, l);
     if (l < N) {
         for (int kk = 0; kk <= l; ++kk) {
-            double v = w.R()[l + kk * w.LDJ];
+            double v = w.R()[l + kk * w.ldj()];
             G_out[(int64_t)(l + kk * N) * B + s] = v;
             G_out[(int64_t)(kk + l * N) * B + s] = v;
         }
@@ -209,7 +225,7 @@ __global__ __launch_bounds__(64) void k_cost(Prob pb, int64_t B, const double* r
 }
 
 // getWLc.m:9-59 materialised (for parity only; the hot path never builds it)
-template <int P>
+template <int P, int NN>
 __global__ __launch_bounds__(64) void k_getwlc(Prob pb, int64_t B, const double* rho, double* W, double* L,
                                                double* c) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -218,7 +234,7 @@ __global__ __launch_bounds__(64) void k_getwlc(Prob pb, int64_t B, const double*
     const int64_t s = (int64_t)blockIdx.x * G + g;
     const int N = pb.N, m = 6 * N + 4;
     if (s >= B) return;
-    WS w = ws_carve(smem + g * ws_bytes(N), N);
+    auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
     for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[(int64_t)e * B + s];
     NTM_WSYNC();
     lift_phase<P>(pb, w, l);
@@ -241,7 +257,7 @@ __global__ __launch_bounds__(64) void k_getwlc(Prob pb, int64_t B, const double*
                 if (cc == 0) Wr0 = -sg; else Wr1 = -sg;
             } else {
                 int r = 2 * (i - 1) + cc;
-                for (int j = 0; j < N; ++j) L[((int64_t)row + (int64_t)j * m) * B + s] = sg * w.Gt()[r + j * w.LDG];
+                for (int j = 0; j < N; ++j) L[((int64_t)row + (int64_t)j * m) * B + s] = sg * ((r >= 2 * j) ? w.gt(r, j) : 0.0);
                 Wr0 = -sg * w.Phi()[4 * (i - 1) + cc];
                 Wr1 = -sg * w.Phi()[4 * (i - 1) + 2 + cc];
                 cr -= sg * w.Lam()[r];
@@ -254,7 +270,7 @@ __global__ __launch_bounds__(64) void k_getwlc(Prob pb, int64_t B, const double*
 }
 
 // quadprog stand-in on explicit data (dense rows)
-template <int P>
+template <int P, int NN>
 __global__ __launch_bounds__(64) void k_qp(int64_t B, int N, int m, const double* G_in, const double* F_in,
                                            const double* Lin, const double* b, double* U, int32_t* exitflag,
                                            int32_t* iters) {
@@ -263,12 +279,13 @@ __global__ __launch_bounds__(64) void k_qp(int64_t B, int N, int m, const double
     const int g = threadIdx.x / P, l = threadIdx.x % P;
     const int64_t s = (int64_t)blockIdx.x * G + g;
     if (s >= B) return;
-    const int wsb = ws_bytes(N) + ((m * 8 + 15) & ~15);
+    const int wsb = ws_bytes(N) + ((m * 8 + 15) & ~15) + N * ldj_of(N) * 8;
     char* base = smem + g * wsb;
-    WS w = ws_carve(base, N);
+    auto w = ws_carve<NN>(base, N);
     double* rnrm = reinterpret_cast<double*>(base + ws_bytes(N));
+    double* gsave = rnrm + ((m + 1) & ~1);     // copy of G~ for the polish (N x LDJ)
     if (l < N) {
-        for (int kk = 0; kk <= l; ++kk) w.R()[l + kk * w.LDJ] = G_in[((int64_t)l + (int64_t)kk * N) * B + s];
+        for (int kk = 0; kk <= l; ++kk) w.R()[l + kk * w.ldj()] = G_in[((int64_t)l + (int64_t)kk * N) * B + s];
         w.F()[l] = F_in[(int64_t)l * B + s];
     }
     for (int i = l; i < m; i += P) w.aflag()[i] = 0;
@@ -283,13 +300,13 @@ __global__ __launch_bounds__(64) void k_qp(int64_t B, int N, int m, const double
         else if (code & 2) flag = NTM_EXIT_INFEASIBLE;
         else {
             // keep G~ for the polish (w.Gt() is unused without a lifted model)
-            if (l < N) for (int j = 0; j <= l; ++j) w.Gt()[l + j * w.LDJ] = w.R()[l + j * w.LDJ];
+            if (l < N) for (int j = 0; j <= l; ++j) gsave[l + j * w.ldj()] = w.R()[l + j * w.ldj()];
             NTM_WSYNC();
-            flag = gi_solve<P, DenseRows>(w, m > 0 ? &rows : nullptr, m, l, &its, &q);
+            flag = gi_solve<P, DenseRows, decltype(w)>(w, m > 0 ? &rows : nullptr, m, l, &its, &q);
         }
     }
     if (flag == NTM_EXIT_OPTIMAL) {
-        (void)polish_phase<P, DenseRows>(Prob{}, w, &rows, q, l, w.Gt(), false, false, nullptr);
+        (void)polish_phase<P, DenseRows, decltype(w)>(Prob{}, w, &rows, q, l, gsave, false, false, nullptr);
     } else if (l < N) {
         w.U()[l] = (flag == NTM_EXIT_MAXITER) ? w.V()[l] * w.D()[l] : 0.0;
     }
@@ -336,7 +353,18 @@ Prob make_prob(const ntm_physics* p, const ntm_config* c) {
     return pb;
 }
 
-int lanes_for(int N) { return N <= 16 ? 16 : (N <= 32 ? 32 : 64); }
+int lanes_for(int N) {
+    // lanes per scenario: the smallest power of two >= N (NTM_LANES=64 forces one scenario per wave)
+    static int forced = [] {
+        const char* e = std::getenv("NTM_LANES");
+        return e ? std::atoi(e) : 0;
+    }();
+    // measured on MI355X (N=20): one scenario per wave (P = 64) beats two per wave
+    // (P = 32): every group decision becomes wave-uniform (scalar branches)
+    int p = N <= 16 ? 16 : 64;
+    if (forced == 16 || forced == 32 || forced == 64) p = forced < N ? 64 : forced;
+    return p;
+}
 
 }  // namespace
 
@@ -385,37 +413,47 @@ int set_lds(ntm_ctx* ctx, K kern, size_t lds) {
     return NTM_OK;
 }
 
-template <int P>
+template <int P, int NN>
 int launch_step(ntm_ctx* ctx, const Prob& pb, int64_t B, const double* x_k, double* rho, double* U_old,
                 double* U, double* x_pred, double* x_next, int32_t* exitflag, int32_t* inner_iters,
                 hipStream_t st) {
     constexpr int G = 64 / P;
     size_t lds = (size_t)G * ws_bytes(pb.N);
-    int rc = set_lds(ctx, k_mpc_step<P>, lds);
+    int rc = set_lds(ctx, k_mpc_step<P, NN>, lds);
     if (rc) return rc;
     int64_t blocks = (B + G - 1) / G;
     if (blocks == 0) return NTM_OK;
-    hipLaunchKernelGGL(k_mpc_step<P>, dim3((unsigned)blocks), dim3(64), lds, st, pb, B, x_k, rho, U_old, U,
+    hipLaunchKernelGGL((k_mpc_step<P, NN>), dim3((unsigned)blocks), dim3(64), lds, st, pb, B, x_k, rho, U_old, U,
                        x_pred, x_next, exitflag, inner_iters);
     return check_hip(ctx, hipGetLastError(), "k_mpc_step launch");
 }
 
-template <int P>
+template <int P, int NN>
 int launch_run(ntm_ctx* ctx, const Prob& pb, int64_t B, int k_sim, const double* x0, double* xk, double* uk,
                double* Uk, double* wpred, int32_t* exitflag, int32_t* inner_iters, hipStream_t st) {
     constexpr int G = 64 / P;
     size_t lds = (size_t)G * ws_bytes(pb.N);
-    int rc = set_lds(ctx, k_mpc_run<P>, lds);
+    int rc = set_lds(ctx, k_mpc_run<P, NN>, lds);
     if (rc) return rc;
     int64_t blocks = (B + G - 1) / G;
     if (blocks == 0) return NTM_OK;
-    hipLaunchKernelGGL(k_mpc_run<P>, dim3((unsigned)blocks), dim3(64), lds, st, pb, B, k_sim, x0, xk, uk, Uk,
+    hipLaunchKernelGGL((k_mpc_run<P, NN>), dim3((unsigned)blocks), dim3(64), lds, st, pb, B, k_sim, x0, xk, uk, Uk,
                        wpred, exitflag, inner_iters);
     return check_hip(ctx, hipGetLastError(), "k_mpc_run launch");
 }
 
-#define NTM_DISPATCH_P(N, CALL) \
-    (lanes_for(N) == 16 ? CALL(16) : (lanes_for(N) == 32 ? CALL(32) : CALL(64)))
+// hot-path dispatch: compile-time horizons for the BASELINE configs (N = 10,
+// 20, 50), a runtime-N kernel for every other horizon
+bool force_generic() {
+    static bool g = std::getenv("NTM_GENERIC") != nullptr;
+    return g;
+}
+#define NTM_DISPATCH_P(N, CALL)                                                     \
+    (force_generic() ? (lanes_for(N) == 16 ? CALL(16, 0) : (lanes_for(N) == 32 ? CALL(32, 0) : CALL(64, 0))) \
+    : lanes_for(N) == 16 ? ((N) == 10 ? CALL(16, 10) : CALL(16, 0))                  \
+                        : (lanes_for(N) == 32 ? CALL(32, 0)                          \
+                                              : ((N) == 20 ? CALL(64, 20)            \
+                                                           : ((N) == 50 ? CALL(64, 50) : CALL(64, 0)))))
 
 struct DevBuf {
     ntm_ctx* ctx;
@@ -511,6 +549,24 @@ void ntm_ctx_destroy(ntm_ctx* ctx) {
 
 const char* ntm_last_error(const ntm_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+// Diagnostic builds (-DNTM_STAMPS) only: copy (and optionally reset) the
+// per-phase cycle totals; returns NTM_E_UNSUPPORTED in production builds.
+int ntm_debug_stamps(unsigned long long* out16, int reset) {
+#ifdef NTM_STAMPS
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(ntm::ntm_stamps), 16 * sizeof(unsigned long long)) != hipSuccess)
+        return NTM_E_DEVICE;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(ntm::ntm_stamps), z, sizeof z) != hipSuccess) return NTM_E_DEVICE;
+    }
+    return NTM_OK;
+#else
+    (void)out16;
+    (void)reset;
+    return NTM_E_UNSUPPORTED;
+#endif
+}
+
 int ntm_ctx_set_stats(ntm_ctx* ctx, int32_t* dev_stats) {
     if (!ctx) return NTM_E_INVALID;
     ctx->stats = dev_stats;
@@ -528,7 +584,7 @@ int ntm_mpc_step_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config*
     Prob pb = make_prob(phys, cfg);
     pb.stats = ctx->stats;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#define CALL(P) launch_step<P>(ctx, pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, st)
+#define CALL(P, NN) launch_step<P, NN>(ctx, pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, st)
     return NTM_DISPATCH_P(cfg->N, CALL);
 #undef CALL
 }
@@ -583,7 +639,7 @@ int ntm_mpc_run_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* 
     Prob pb = make_prob(phys, cfg);
     pb.stats = ctx->stats;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#define CALL(P) launch_run<P>(ctx, pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, st)
+#define CALL(P, NN) launch_run<P, NN>(ctx, pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, st)
     return NTM_DISPATCH_P(cfg->N, CALL);
 #undef CALL
 }
@@ -651,14 +707,14 @@ int ntm_AB_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, 
         size_t lds_ = (size_t)G_ * ws_bytes(N);                                                     \
         unsigned blocks_ = (unsigned)(((B) + G_ - 1) / G_);                                         \
         if (P_ == 16) {                                                                             \
-            if ((rc = set_lds(ctx, KERN<16>, lds_))) return rc;                                     \
-            hipLaunchKernelGGL(KERN<16>, dim3(blocks_), dim3(64), lds_, st, __VA_ARGS__);           \
+            if ((rc = set_lds(ctx, KERN<16, 0>, lds_))) return rc;                                     \
+            hipLaunchKernelGGL((KERN<16, 0>), dim3(blocks_), dim3(64), lds_, st, __VA_ARGS__);           \
         } else if (P_ == 32) {                                                                      \
-            if ((rc = set_lds(ctx, KERN<32>, lds_))) return rc;                                     \
-            hipLaunchKernelGGL(KERN<32>, dim3(blocks_), dim3(64), lds_, st, __VA_ARGS__);           \
+            if ((rc = set_lds(ctx, KERN<32, 0>, lds_))) return rc;                                     \
+            hipLaunchKernelGGL((KERN<32, 0>), dim3(blocks_), dim3(64), lds_, st, __VA_ARGS__);           \
         } else {                                                                                    \
-            if ((rc = set_lds(ctx, KERN<64>, lds_))) return rc;                                     \
-            hipLaunchKernelGGL(KERN<64>, dim3(blocks_), dim3(64), lds_, st, __VA_ARGS__);           \
+            if ((rc = set_lds(ctx, KERN<64, 0>, lds_))) return rc;                                     \
+            hipLaunchKernelGGL((KERN<64, 0>), dim3(blocks_), dim3(64), lds_, st, __VA_ARGS__);           \
         }                                                                                           \
     } while (0)
 
@@ -697,20 +753,20 @@ int ntm_qp_device(ntm_ctx* ctx, int64_t B, int32_t N, int32_t m, const double* G
     if (B < 0) return fail(ctx, NTM_E_INVALID, "negative batch");
     if (B == 0) return NTM_OK;
     int P = lanes_for(N), Gs = 64 / P;
-    size_t per = (size_t)ws_bytes(N) + ((m * 8 + 15) & ~15);
+    size_t per = (size_t)ws_bytes(N) + ((m * 8 + 15) & ~15) + (size_t)N * ldj_of(N) * 8;
     size_t lds = Gs * per;
     unsigned blocks = (unsigned)((B + Gs - 1) / Gs);
     hipStream_t st = (hipStream_t)stream;
     int rc;
     if (P == 16) {
-        if ((rc = set_lds(ctx, k_qp<16>, lds))) return rc;
-        hipLaunchKernelGGL(k_qp<16>, dim3(blocks), dim3(64), lds, st, B, N, m, G, F, Lin, b, U, exitflag, iters);
+        if ((rc = set_lds(ctx, k_qp<16, 0>, lds))) return rc;
+        hipLaunchKernelGGL((k_qp<16, 0>), dim3(blocks), dim3(64), lds, st, B, N, m, G, F, Lin, b, U, exitflag, iters);
     } else if (P == 32) {
-        if ((rc = set_lds(ctx, k_qp<32>, lds))) return rc;
-        hipLaunchKernelGGL(k_qp<32>, dim3(blocks), dim3(64), lds, st, B, N, m, G, F, Lin, b, U, exitflag, iters);
+        if ((rc = set_lds(ctx, k_qp<32, 0>, lds))) return rc;
+        hipLaunchKernelGGL((k_qp<32, 0>), dim3(blocks), dim3(64), lds, st, B, N, m, G, F, Lin, b, U, exitflag, iters);
     } else {
-        if ((rc = set_lds(ctx, k_qp<64>, lds))) return rc;
-        hipLaunchKernelGGL(k_qp<64>, dim3(blocks), dim3(64), lds, st, B, N, m, G, F, Lin, b, U, exitflag, iters);
+        if ((rc = set_lds(ctx, k_qp<64, 0>, lds))) return rc;
+        hipLaunchKernelGGL((k_qp<64, 0>), dim3(blocks), dim3(64), lds, st, B, N, m, G, F, Lin, b, U, exitflag, iters);
     }
     return check_hip(ctx, hipGetLastError(), "k_qp");
 }

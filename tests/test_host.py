@@ -30,11 +30,13 @@ def test_library_exports_every_declared_symbol():
     assert set(EXPORTS) == set(names)
 
 
-def test_library_is_gfx950_code_object():
+def test_library_is_gfx950_code_object(tmp_path):
+    import shutil
     import subprocess
-    lib = ROOT / "mpc-ntm-control_amd" / "lib" / "libntm_mpc.so"
+    lib = tmp_path / "libntm_mpc.so"          # llvm-objdump extracts bundles next to its input
+    shutil.copy(ROOT / "mpc-ntm-control_amd" / "lib" / "libntm_mpc.so", lib)
     out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)], capture_output=True,
-                         text=True)
+                         text=True, cwd=tmp_path)
     assert "gfx950" in (out.stdout + out.stderr)
 
 

@@ -1,0 +1,27 @@
+"""Diagnostic (not a test): per-phase cycle breakdown of the fused step kernel
+using the -DNTM_STAMPS build (lib/libntm_mpc_diag.so)."""
+import ctypes as C, os, sys, time
+os.environ["NTM_MPC_LIB"] = os.path.join(os.path.dirname(__file__), "..", "mpc-ntm-control_amd", "lib", "libntm_mpc_diag.so")
+sys.path[:0] = [os.path.join(os.path.dirname(__file__), ".."), os.path.join(os.path.dirname(__file__), "..", "mpc-ntm-control_amd")]
+import torch, ntm_mpc
+from ntm_mpc import NtmMpc, Config
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
+cfg = Config(N=20, mode=2)
+ctl = NtmMpc(config=cfg)
+lib = ntm_mpc.load()
+buf = (C.c_ulonglong * 16)()
+x = torch.tensor(ntm_mpc.scenarios_x0(0, B), device="cuda")
+rho, uo = ctl.initial_state(x, cfg)
+out = ctl.step(x, rho, uo, cfg); torch.cuda.synchronize()
+x = out["x_next"].clone()
+lib.ntm_debug_stamps(buf, 1)
+t = time.time()
+out = ctl.step(x, rho, uo, cfg); torch.cuda.synchronize()
+dt = time.time() - t
+assert lib.ntm_debug_stamps(buf, 1) == 0
+names = "lift cost scale cand regram gi polish roll gi_fact gi_check gi_dir gi_add gi_drop".split()
+tot = sum(buf[i] for i in range(8))
+print(f"B={B} step {dt*1e3:.1f} ms; cycles per wave-step by phase (s_memtime):")
+for i, n in enumerate(names):
+    print(f"  {n:9s} {buf[i]/B:12.0f}  {100*buf[i]/tot:5.1f}%")
+print(f"per wave-step: check calls {buf[13]/B:.1f}, candidate tries {buf[14]/B:.2f}, hits {buf[15]/B:.2f}")
