@@ -267,7 +267,8 @@ struct WS {
     // double offsets of each array (n() is launch-uniform, so these fold to scalar math)
     __device__ __forceinline__ int oJ() const { return 14 * n() + n() * (n() + 1); }
     __device__ __forceinline__ int oR() const { return oJ() + n() * ldj(); }
-    __device__ __forceinline__ int oV() const { return oR() + (n() + 1) * ldj(); }   // start of the vector block
+    __device__ __forceinline__ int oT() const { return oR() + (n() + 1) * ldj(); }
+    __device__ __forceinline__ int oV() const { return oT() + n() * ldj(); }         // start of the vector block
     __device__ __forceinline__ double* rho() const { return base; }                 // 3N (3xN col-major)
     __device__ __forceinline__ double* a11() const { return base + 3 * n(); }         // n()
     __device__ __forceinline__ double* a21() const { return base + 4 * n(); }         // n()
@@ -283,6 +284,9 @@ struct WS {
     // R: n() rows x (n()+1) columns col-major; the polish keeps its Schur complement
     // K in the strict upper triangle: K(a, c), a >= c, at R[c + (a+1) ldj()]
     __device__ __forceinline__ double* R() const { return base + oR(); }
+    // T = R^{-1} of the GI factorisation (upper triangular, row-major n() x ldj();
+    // zero outside the leading q x q block), so the dual direction is a matvec
+    __device__ __forceinline__ double* T() const { return base + oT(); }
     __device__ __forceinline__ double* rn() const { return base + oV(); }           // 2N state-row norms
     __device__ __forceinline__ double* F() const { return base + oV() + 2 * n(); }    // n()  F~
     __device__ __forceinline__ double* D() const { return base + oV() + 3 * n(); }    // n()  Jacobi scaling
@@ -296,7 +300,7 @@ struct WS {
     __device__ __forceinline__ double* xp() const { return base + oV() + 11 * n() + 1; }   // 2(n()+1) rollout
     __device__ __forceinline__ double* U() const { return base + oV() + 13 * n() + 3; }    // n()
     __device__ __forceinline__ double* Uold() const { return base + oV() + 14 * n() + 3; } // n()
-    __device__ __forceinline__ double* rinv() const { return base + oV() + 15 * n() + 3; }  // N: 1/R(b,b) of the GI R
+    __device__ __forceinline__ double* dr() const { return base + oV() + 15 * n() + 3; }    // N: d masked to b < q (GI)
     // per-QP constants hoisted out of the solver loops
     __device__ __forceinline__ double* vlo() const { return base + oV() + 16 * n() + 3; }   // N: umin/D_j
     __device__ __forceinline__ double* vhi() const { return base + oV() + 17 * n() + 3; }   // N: umax/D_j
@@ -317,7 +321,7 @@ struct WS {
 
 __host__ __device__ inline int ldj_of(int N) { return N | 1; }
 __host__ __device__ inline int ws_doubles(int N) {
-    return 14 * N + N * (N + 1) + N * ldj_of(N) + (N + 1) * ldj_of(N) + 23 * N + 3;
+    return 14 * N + N * (N + 1) + 2 * N * ldj_of(N) + (N + 1) * ldj_of(N) + 23 * N + 3;
 }
 __host__ __device__ inline int ws_bytes(int N) {
     int b = ws_doubles(N) * 8 + 6 * (N + 1) * 4 + N + (6 * NTM_MAX_N + 4);
@@ -678,7 +682,12 @@ struct StructRows {
                     int jmax = r >> 1;
                     const double* gr = w.Gt() + r;           // gt(r, j) = gr[gidx(0, j)]
                     double xh = 0.0;
-                    for (int j = 0; j <= jmax; ++j) xh += gr[w.gidx(0, j)] * w.U()[j];
+                    // fixed trip count (unrolls); entries j > jmax are masked.  The packed
+                    // reads stay inside Gt: gidx(0, j) + r = j(2N-j-1) + r < N(N+1)
+                    for (int j = 0; j < N; ++j) {
+                        const double g = gr[w.gidx(0, j)];
+                        xh += (j <= jmax ? g : 0.0) * w.U()[j];
+                    }
                     const double er = w.e()[r];
                     xh += er;
                     int c = r & 1, i = jmax + 1;
@@ -879,6 +888,7 @@ __device__ int gi_solve(const W& w, const Rows* rows, int nrows, int l, int* ite
     }
     NTM_ACC(ST_GI_FACT, tg);
     if (!rows) return NTM_EXIT_OPTIMAL;
+    if (l < N) for (int b = 0; b < N; ++b) w.T()[l * LDJ + b] = 0.0;
     const int max_iter = 10 * (N + nrows) + 50;
     int q = 0, it = 0;
     for (;;) {
@@ -910,17 +920,17 @@ __device__ int gi_solve(const W& w, const Rows* rows, int nrows, int l, int* ite
             } else if (l < N) {
                 for (int i = 0; i < N; ++i) dl += w.J()[i * LDJ + l] * w.np()[i];
             }
-            if (l < N) w.d()[l] = dl;
+            // d split at q: d2 = d[q:N] (w.d) and d1 = d[0:q] (w.dr), zero elsewhere, so
+            // both matvecs run full fixed-length rows (unrolled, loads batched)
+            if (l < N) { w.d()[l] = (l >= q) ? dl : 0.0; w.dr()[l] = (l < q) ? dl : 0.0; }
             NTM_WSYNC();
-            // z = J2 d2 (primal direction)
-            double zl = 0.0;
-            if (l < N) for (int k2 = q; k2 < N; ++k2) zl += w.J()[l * LDJ + k2] * w.d()[k2];
-            // r = R^{-1} d1 (negative dual direction), back substitution
-            double acc = (l < q) ? dl : 0.0, rl = 0.0;
-            for (int b = q - 1; b >= 0; --b) {
-                double rb = gbcast<P>(acc, b) * w.rinv()[b];
-                if (l == b) rl = rb;
-                if (l < b) acc -= w.R()[l + b * LD] * rb;
+            // z = J2 d2 (primal direction) and r = T d1 = R^{-1} d1 (negative dual direction)
+            double zl = 0.0, rl = 0.0;
+            if (l < N) {
+#pragma unroll 4
+                for (int k2 = 0; k2 < N; ++k2) zl += w.J()[l * LDJ + k2] * w.d()[k2];
+#pragma unroll 4
+                for (int b = 0; b < N; ++b) rl += w.T()[l * LDJ + b] * w.dr()[b];
             }
             // partial (dual) step length t1
             double ratio = (l < q && rl > 0.0) ? w.uu()[l] / rl : kInf;
@@ -952,20 +962,22 @@ __device__ int gi_solve(const W& w, const Rows* rows, int nrows, int l, int* ite
                     if (q < N - 1 && nrm > 0.0) {
                         h = (dqv >= 0.0) ? -nrm : nrm;
                         double vl = (l == q) ? dl - h : ((l > q && l < N) ? dl : 0.0);
-                        if (l < N) w.hv()[l] = vl;
+                        if (l < N) w.hv()[l] = vl;          // zero for l < q
                         double vtv = gsum<P>(vl * vl);
                         NTM_WSYNC();
                         if (l < N) {
                             double dot = 0.0;
-                            for (int k2 = q; k2 < N; ++k2) dot += w.J()[l * LDJ + k2] * w.hv()[k2];
+                            for (int k2 = 0; k2 < N; ++k2) dot += w.J()[l * LDJ + k2] * w.hv()[k2];
                             double f = 2.0 * dot / vtv;
                             for (int k2 = q; k2 < N; ++k2) w.J()[l * LDJ + k2] -= f * w.hv()[k2];
                         }
                     }
-                    if (l < q) w.R()[l + q * LD] = dl;
+                    // R gains column q = [d1; h]; T = R^{-1} gains column q = [-r/h; 1/h]
+                    const double ih = 1.0 / h;
+                    if (l < q) { w.R()[l + q * LD] = dl; w.T()[l * LDJ + q] = -rl * ih; }
                     if (l == q) {
                         w.R()[q + q * LD] = h;
-                        w.rinv()[q] = 1.0 / h;
+                        w.T()[q * LDJ + q] = ih;
                         w.act()[q] = p;
                         w.aflag()[p] = 1;
                         w.uu()[q] = upq;
@@ -1004,15 +1016,28 @@ __device__ int gi_solve(const W& w, const Rows* rows, int nrows, int l, int* ite
                     double nr = cc * r1 + ss * r2;
                     w.R()[j + l * LD] = nr;
                     w.R()[(j + 1) + l * LD] = (l == j) ? 0.0 : (-ss * r1 + cc * r2);
-                    if (l == j) w.rinv()[j] = 1.0 / nr;
                 }
                 if (l < N) {
                     double j1 = w.J()[l * LDJ + j], j2 = w.J()[l * LDJ + j + 1];
                     w.J()[l * LDJ + j] = cc * j1 + ss * j2;
                     w.J()[l * LDJ + j + 1] = -ss * j1 + cc * j2;
                 }
+                if (l < q) {   // T <- T G_j' (the columns rotate like J's)
+                    double t1v = w.T()[l * LDJ + j], t2v = w.T()[l * LDJ + j + 1];
+                    w.T()[l * LDJ + j] = cc * t1v + ss * t2v;
+                    w.T()[l * LDJ + j + 1] = -ss * t1v + cc * t2v;
+                }
                 NTM_WSYNC();
             }
+            // R'^{-1} = (T Q) without row l0 and column q-1.  Lane c owns column c:
+            // rows l0+1..q-1 move up one; the discarded column q-1 is cleared
+            if (l < q - 1) {
+                for (int a = l0; a < q - 1; ++a) w.T()[a * LDJ + l] = w.T()[(a + 1) * LDJ + l];
+                w.T()[(q - 1) * LDJ + l] = 0.0;
+            } else if (l == q - 1) {
+                for (int a = 0; a < q; ++a) w.T()[a * LDJ + l] = 0.0;
+            }
+            NTM_WSYNC();
             --q;
             NTM_ACC(ST_GI_DROP, tg);
         }
