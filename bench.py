@@ -90,6 +90,7 @@ def main():
     import ntm_mpc
     from ntm_mpc import Config, NtmMpc
     from ntm_mpc import flops as FL
+    from ntm_mpc.api import STATS_ROWS
 
     B, N, K, W = args.batch, args.N, args.steps, args.warmup
     cfg = Config(N=N, mode=args.mode)
@@ -109,15 +110,15 @@ def main():
     for i in range(W):
         x = one_step(i, x)["x_next"].clone()
     # instrumentation pass (untimed, separate launch on a copy of the state)
-    stats = torch.zeros(4, B, dtype=torch.int32, device=dev)
+    stats = torch.zeros(STATS_ROWS, B, dtype=torch.int32, device=dev)
     rho_s, uo_s = rho.clone(), U_old.clone()
     ctl.set_stats(stats)
     ctl.step(x, rho_s, uo_s, cfg)
     ctl.set_stats(None)
     torch.cuda.synchronize()
     st = stats.double().sum(dim=1).cpu().numpy()
-    qps = st[0] / B
-    Kgi, qact, sgen = st[1] / st[0], st[2] / st[0], st[3] / st[0]
+    qps, Kgi, tries, giruns = st[0] / B, st[1] / B, st[4] / B, st[5] / B     # per MPC step
+    qact, sgen = st[2] / st[0], st[3] / st[0]                                 # per QP
     del rho_s, uo_s
 
     hist_u = torch.empty(K, B, dtype=torch.float64, device=dev)
@@ -155,7 +156,7 @@ def main():
     iters = out["inner_iters"].double().mean().item()
 
     value = world * B * K / elapsed
-    flop_step = FL.per_step(N, args.mode, qps, Kgi, qact, sgen)
+    flop_step = FL.per_step(N, args.mode, qps, tries, giruns, Kgi, qact, sgen)
     achieved = flop_step * B / (kern_ms * 1e-3) / 1e12
     traffic = None
     prof = ROOT / "profiles" / "traffic_r01.json"
@@ -185,11 +186,12 @@ def main():
                    "parallelism": f"scenario-sharded x{world} (weak), end-of-batch all_gather"},
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": "k_mpc_step<32>", "kernel_avg_ms": kern_ms,
+                     "kernel": ctl.step_kernel_name(B, cfg), "kernel_avg_ms": kern_ms,
                      "flop_per_step": flop_step,
                      "hbm_algorithmic_bytes_per_launch": FL.hbm_bytes_per_step(N) * B,
                      "note": "fp64 VALU work; peak = MI355X dense fp64 (vector == matrix rate)"},
-        "solver": {"inner_iters_mean": iters, "qp_per_step": qps, "gi_iters_per_qp": Kgi,
+        "solver": {"inner_iters_mean": iters, "qp_per_step": qps, "warm_verify_per_step": tries,
+                   "gi_solves_per_step": giruns, "gi_iters_per_step": Kgi,
                    "active_rows_per_qp": qact, "state_rows_per_qp": sgen, "optimal_frac": n_opt / B},
     }
     if rank == 0 and not args.no_cpu:

@@ -84,13 +84,19 @@ typedef struct ntm_ctx ntm_ctx;
 int ntm_ctx_create(ntm_ctx** out, int32_t device);
 void ntm_ctx_destroy(ntm_ctx* ctx);
 const char* ntm_last_error(const ntm_ctx* ctx);
-/* Optional instrumentation: device array of 4*B int32 (SoA) that subsequent
- * step/run launches ACCUMULATE into: QP solves, Goldfarb-Idnani iterations,
- * final active rows, general (state) active rows.  NULL disables. */
+/* Optional instrumentation: device array of NTM_STATS_ROWS*B int32 (SoA, row
+ * k of scenario s at [k*B + s]) that subsequent step/run launches ACCUMULATE
+ * into: 0 QP solves, 1 Goldfarb-Idnani iterations, 2 final active rows,
+ * 3 general (state) active rows, 4 warm-start candidate verifications,
+ * 5 full Goldfarb-Idnani solves.  NULL disables. */
+#define NTM_STATS_ROWS 6
 int ntm_ctx_set_stats(ntm_ctx* ctx, int32_t* dev_stats);
 /* Diagnostic builds only: per-phase s_memtime cycle totals (16 counters);
  * NTM_E_UNSUPPORTED in production builds. */
 int ntm_debug_stamps(unsigned long long* out16, int reset);
+/* Launch shape the step/run kernels use for horizon N: lanes per scenario
+ * (16/32/64) and the compile-time horizon of the specialisation (0 = generic). */
+int ntm_step_launch_info(int32_t N, int32_t* lanes, int32_t* horizon_template);
 
 /* ---- time-step level: the drop-in for NTM_MPC_Sim.m:94-130 ------------ */
 /* One MPC step for B scenarios.  In/out state per scenario:

@@ -1528,7 +1528,7 @@ __device__ __forceinline__ void plant_step(const Prob& pb, double x0, double x1,
 // ---------------------------------------------------------------------------
 template <int P, class W>
 __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l, int* qp_iters,
-                        int* q_out, int* ns_out, int slot) {
+                        int* q_out, int* ns_out, int slot, int* n_try = nullptr, int* n_girun = nullptr) {
     const int N = w.n();
     NTM_T0(tq);
     lift_phase<P>(pb, w, l);
@@ -1561,6 +1561,7 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
             const int cq = uni<P>(cand[N]);
             if (cq >= 0) {
                 NTM_CNT(CN_CAND);
+                if (n_try) ++*n_try;
                 if (l < cq) w.act()[l] = cand[l];
                 NTM_WSYNC();
                 if (polish_compact<P>(pb, w, &rows, cq, l, true, &ns)) {
@@ -1576,6 +1577,7 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                     flag = NTM_EXIT_NONFINITE;
                 } else {
                     NTM_ACC(ST_REGRAM, tq);
+                    if (n_girun) ++*n_girun;
                     flag = gi_solve<P, StructRows, W>(w, pb.mode == NTM_MODE_NONE ? nullptr : &rows, nrows, l,
                                                       qp_iters, &q);
                     NTM_ACC(ST_GI, tq);

@@ -37,15 +37,24 @@ __device__ __forceinline__ void load_state(const W& w, int64_t B, int64_t s, con
     NTM_WSYNC();
 }
 
+// XCD-aware block order (bijective): blocks are dealt round-robin over the 8
+// XCDs, so block b is given the k-th slot of XCD b%8's contiguous range of
+// scenario blocks.  Neighbouring scenarios share the cache lines of the SoA
+// (scenario-minor) state arrays; this keeps each line's users on one L2.
+__device__ __forceinline__ int64_t xcd_swizzle(int64_t b, int64_t nb) {
+    const int64_t q = nb >> 3, r = nb & 7, x = b & 7, k = b >> 3;
+    return x * q + (x < r ? x : r) + k;
+}
+
 // one MPC step on LDS-resident state; returns exit flag, sets *iters
 template <int P, class W>
 __device__ int mpc_step_dev(const Prob& pb, const W& w, double x0, double x1, int l, int* iters,
                             int64_t B = 0, int64_t s = 0) {
     int flag = NTM_EXIT_OPTIMAL, it;
-    int n_qp = 0, n_gi = 0, n_act = 0, n_gen = 0;
+    int n_qp = 0, n_gi = 0, n_act = 0, n_gen = 0, n_try = 0, n_girun = 0;
     for (it = 1; it <= pb.i_sim; ++it) {
         int qi = 0, qa = 0, ns = 0;
-        flag = qp_phase<P>(pb, w, x0, x1, l, &qi, &qa, &ns, (it - 1) & 1);
+        flag = qp_phase<P>(pb, w, x0, x1, l, &qi, &qa, &ns, (it - 1) & 1, &n_try, &n_girun);
         ++n_qp;
         n_gi += qi;
         n_act += qa;
@@ -61,6 +70,8 @@ __device__ int mpc_step_dev(const Prob& pb, const W& w, double x0, double x1, in
         pb.stats[B + s] += n_gi;
         pb.stats[2 * B + s] += n_act;
         pb.stats[3 * B + s] += n_gen;
+        pb.stats[4 * B + s] += n_try;
+        pb.stats[5 * B + s] += n_girun;
     }
     return flag;
 }
@@ -77,7 +88,7 @@ __global__ __launch_bounds__(64, NTM_HOT_WAVES_PER_EU) void k_mpc_step(Prob pb, 
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int G = 64 / P;
     const int g = threadIdx.x / P, l = threadIdx.x % P;
-    const int64_t s = (int64_t)blockIdx.x * G + g;
+    const int64_t s = xcd_swizzle(blockIdx.x, gridDim.x) * G + g;
     const int N = NN > 0 ? NN : pb.N;
     NTM_STAMPS_INIT();
     if (s >= B) return;
@@ -111,7 +122,7 @@ __global__ __launch_bounds__(64, NTM_HOT_WAVES_PER_EU) void k_mpc_run(Prob pb, i
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int G = 64 / P;
     const int g = threadIdx.x / P, l = threadIdx.x % P;
-    const int64_t s = (int64_t)blockIdx.x * G + g;
+    const int64_t s = xcd_swizzle(blockIdx.x, gridDim.x) * G + g;
     const int N = NN > 0 ? NN : pb.N;
     if (s >= B) return;
     auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
@@ -587,6 +598,13 @@ int ntm_mpc_step_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config*
 #define CALL(P, NN) launch_step<P, NN>(ctx, pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, st)
     return NTM_DISPATCH_P(cfg->N, CALL);
 #undef CALL
+}
+
+int ntm_step_launch_info(int32_t N, int32_t* lanes, int32_t* horizon_template) {
+    if (N < 1 || N > NTM_MAX_N || !lanes || !horizon_template) return NTM_E_INVALID;
+#define INFO(P_, NN_) (*lanes = (P_), *horizon_template = (NN_), 0)
+    return NTM_DISPATCH_P(N, INFO);
+#undef INFO
 }
 
 int ntm_mpc_step(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* x_k,

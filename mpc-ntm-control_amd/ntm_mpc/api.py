@@ -32,6 +32,9 @@ from . import _lib as L
 from ._lib import NtmConfig, NtmLibraryError, NtmPhysics
 
 
+STATS_ROWS = 6   # include/ntm_mpc.h NTM_STATS_ROWS
+
+
 @dataclass
 class Physics:
     """Physics constants, NTM_MPC_Sim.m:5-22."""
@@ -143,12 +146,22 @@ class NtmMpc:
         return torch.empty(*shape, dtype=dtype, device=f"cuda:{self.device}")
 
     def set_stats(self, stats: torch.Tensor | None):
-        """Accumulate per-scenario counters (4, B) int32 into ``stats`` during
-        subsequent step/run launches (QP solves, GI iterations, final active
-        rows, state rows in the final active set); None disables."""
+        """Accumulate per-scenario counters (NTM_STATS_ROWS=6, B) int32 into
+        ``stats`` during subsequent step/run launches: QP solves, GI iterations,
+        final active rows, state rows in the final active set, warm-start
+        candidate verifications, full GI solves; None disables."""
         if stats is not None:
+            if stats.dim() != 2 or stats.shape[0] != STATS_ROWS:
+                raise ValueError(f"stats must be ({STATS_ROWS}, B) int32")
             _check_dev(stats, tuple(stats.shape), dtype=torch.int32, name="stats")
         self._raise(self.lib.ntm_ctx_set_stats(self._ctx, _ptr(stats)), "ntm_ctx_set_stats")
+
+    def step_kernel_name(self, B: int, cfg: Config | None = None) -> str:
+        """Name of the fused step kernel specialisation a launch uses (reporting)."""
+        cfg = cfg or self.config
+        lanes, nn = C.c_int32(), C.c_int32()
+        self._raise(self.lib.ntm_step_launch_info(cfg.N, C.byref(lanes), C.byref(nn)), "ntm_step_launch_info")
+        return f"k_mpc_step<P={lanes.value},NN={nn.value}>"
 
     # ------------------------------------------------------------ hot path
     def initial_state(self, x0: torch.Tensor, cfg: Config | None = None):

@@ -100,10 +100,25 @@ def test_ctx_create_without_gpu_is_an_error():
 
 def test_flop_model_monotone():
     from ntm_mpc import flops
-    a = flops.per_step(20, 2, 8, 10, 19, 5)
-    b = flops.per_step(20, 2, 8, 40, 19, 5)
-    assert 0 < a < b
+    # qps, tries, giruns, K (per step); q, s (per QP)
+    a = flops.per_step(20, 2, 8, 6, 2, 60, 19, 5)
+    b = flops.per_step(20, 2, 8, 6, 2, 90, 19, 5)
+    c = flops.per_step(20, 2, 8, 4, 4, 60, 19, 5)        # a full GI solve costs more than a verify
+    assert 0 < a < b and a < c
+    # never above the survey's IPM-based count (6.47e6 flop/step at N=20)
+    assert flops.per_step(20, 2, 10, 0, 10, 400, 20, 10) < 6.47e6
     assert flops.hbm_bytes_per_step(20) == 8 * (2 + 120 + 40 + 20 + 42 + 2) + 8
+
+
+def test_launch_info_dispatch():
+    """The kernel specialisation per horizon (host logic, no GPU needed)."""
+    import ntm_mpc
+    lib = ntm_mpc.load()
+    lanes, nn = C.c_int32(), C.c_int32()
+    for N, want in [(3, (16, 0)), (10, (16, 10)), (20, (64, 20)), (33, (64, 0)), (50, (64, 50))]:
+        assert lib.ntm_step_launch_info(N, C.byref(lanes), C.byref(nn)) == 0
+        assert (lanes.value, nn.value) == want, N
+    assert lib.ntm_step_launch_info(0, C.byref(lanes), C.byref(nn)) != 0
 
 
 def test_product_never_imports_oracle():
