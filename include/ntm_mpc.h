@@ -99,6 +99,15 @@ int ntm_debug_stamps(unsigned long long* out16, int reset);
 int ntm_step_launch_info(int32_t N, int32_t* lanes, int32_t* horizon_template);
 
 /* ---- time-step level: the drop-in for NTM_MPC_Sim.m:94-130 ------------ */
+/* Initial LPV state for x0[2]: rho[3N] = repmat(rho(x0), 1, N)
+ * (NTM_MPC_Sim.m:63-65) and U_old[N] = +Inf (the first convergence test never
+ * passes, D14; the literal Uold = ones(...) at :86 is an implicit-expansion
+ * defect). */
+int ntm_mpc_init(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg,
+                 int64_t B, const double* x0, double* rho, double* U_old);
+int ntm_mpc_init_device(ntm_ctx* ctx, const ntm_physics* phys,
+                        const ntm_config* cfg, int64_t B, const double* x0,
+                        double* rho, double* U_old, void* stream);
 /* One MPC step for B scenarios.  In/out state per scenario:
  *   x_k[2], rho[3N] (3xN col-major: rows rho1,rho2,rho3; carried unshifted,
  *   D20), U_old[N] (persists across steps, D14; +inf on the first step).

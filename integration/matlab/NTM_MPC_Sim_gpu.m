@@ -1,0 +1,52 @@
+function [xk, uk, Uk, exitflag, iters] = NTM_MPC_Sim_gpu(x0, k_sim, cfg, mode)
+%NTM_MPC_SIM_GPU  Drop-in for the controller loop of NTM_MPC_Sim.m (lines 80-131)
+%   on MI355X, for one or many scenarios at once.
+%
+%   [xk, uk, Uk] = NTM_MPC_Sim_gpu(x0, k_sim, cfg)
+%     x0    2-by-B initial states [w; omega], one column per scenario
+%           (the reference's x0, NTM_MPC_Sim.m:34, is the B = 1 case)
+%     k_sim number of time steps (NTM_MPC_Sim.m:80)
+%     cfg   struct of controller settings (N, i_sim, mode, Ts, xmin, xmax,
+%           umin, umax, Q, r, epsilon); omitted fields take the reference's
+%           literals (NTM_MPC_Sim.m:30-88)
+%     mode  'run' (default): the whole closed loop on the device, one call;
+%           'step': one MEX call per time step (the state stays in MATLAB)
+%   Returns the reference's workspace variables with a trailing scenario
+%   dimension: xk 2-by-(k_sim+1)-by-B, uk 1-by-k_sim-by-B, Uk N-by-k_sim-by-B,
+%   plus exitflag / iters (k_sim-by-B, quadprog codes and LPV iterations).
+%
+%   Semantics are the repaired ones of SURVEY.md §2.1 (CANON): Phi_i = A_i
+%   Phi_{i-1}, Gamma_ij = A_i Gamma_{i-1,j}, W/L/c rebuilt each iteration, F
+%   from the current x_k, plant step with +C, Uold = +Inf at start.
+if nargin < 3, cfg = struct(); end
+if nargin < 4, mode = 'run'; end
+if ~isfield(cfg, 'N'), cfg.N = 20; end
+N = cfg.N;
+B = size(x0, 2);
+X0 = x0.';                                   % B-by-2: the ABI's scenario-minor layout
+switch mode
+    case 'run'
+        [XK, UK, UKK, ~, FL, IT] = ntm_mpc_mex('run', X0, k_sim, cfg);
+        xk = permute(reshape(XK, B, 2, k_sim + 1), [2 3 1]);
+        uk = permute(reshape(UK, B, 1, k_sim), [2 3 1]);
+        Uk = permute(reshape(UKK, B, N, k_sim), [2 3 1]);
+        exitflag = FL.';
+        iters = IT.';
+    case 'step'
+        xk = zeros(2, k_sim + 1, B); uk = zeros(1, k_sim, B); Uk = zeros(N, k_sim, B);
+        exitflag = zeros(k_sim, B, 'int32'); iters = zeros(k_sim, B, 'int32');
+        xk(:, 1, :) = reshape(x0, 2, 1, B);
+        [Rho, Uold] = ntm_mpc_mex('init', X0, cfg);   % Rho = repmat(rho(x0),1,N), Uold = +Inf
+        X = X0;
+        for k = 1:k_sim
+            [U, ~, Xn, fl, it, Rho, Uold] = ntm_mpc_mex('step', X, Rho, Uold, cfg);
+            Uk(:, k, :) = reshape(U.', N, 1, B);
+            uk(1, k, :) = reshape(U(:, 1), 1, 1, B);
+            exitflag(k, :) = fl.'; iters(k, :) = it.';
+            X = Xn;
+            xk(:, k + 1, :) = reshape(Xn.', 2, 1, B);
+        end
+    otherwise
+        error('ntm:arg', 'mode must be ''run'' or ''step''');
+end
+end

@@ -1,0 +1,174 @@
+/*
+ * ntm_mpc_mex.c — MATLAB MEX gateway over the C-ABI in include/ntm_mpc.h.
+ *
+ * Replaces, for a batch of B scenarios, the body of the receding-horizon loop
+ * of NTM_MPC_Sim.m (lines 94-130: the LPV iteration, quadprog call and plant
+ * step) or the whole closed loop (lines 80-131).  Build, where MATLAB exists:
+ *
+ *   mex -R2018a -I../../include ntm_mpc_mex.c \
+ *       -L../../mpc-ntm-control_amd/lib -lntm_mpc
+ *
+ * Calls (every batched array is B-by-E: one row per scenario, which is the
+ * ABI's scenario-minor layout [e*B + s] in MATLAB's column-major storage):
+ *
+ *   [U, x_pred, x_next, exitflag, iters, rho, Uold] = ...
+ *       ntm_mpc_mex('step', x_k, rho, Uold, cfg)
+ *         x_k  B-by-2        current state [w, omega]           (xk(:,k)')
+ *         rho  B-by-3N       reshape(Rho, 1, 3N) per scenario   (:63-65,116)
+ *         Uold B-by-N        +Inf on the first step (D14)
+ *   [rho, Uold] = ntm_mpc_mex('init', x0, cfg)                 (:63-65, :86)
+ *   [xk, uk, Uk, wpred, exitflag, iters] = ntm_mpc_mex('run', x0, k_sim, cfg)
+ *   ntm_mpc_mex('close')
+ *
+ * cfg is an optional struct with any of the fields N, i_sim, mode, flags, Ts,
+ * xmin, xmax, umin, umax, Q (2x2), r, epsilon; missing fields take the
+ * reference literals (ntm_config_default).  Library errors become MATLAB
+ * errors (ntm:...); solver outcomes are returned in exitflag (quadprog codes,
+ * NTM_MPC_Sim.m:98-103), never raised.
+ */
+#include <string.h>
+
+#include "mex.h"
+#include "ntm_mpc.h"
+
+static ntm_ctx* g_ctx = NULL;
+
+static void release(void) {
+    if (g_ctx) {
+        ntm_ctx_destroy(g_ctx);
+        g_ctx = NULL;
+    }
+}
+
+static void check(int rc, const char* what) {
+    if (rc != NTM_OK) {
+        mexErrMsgIdAndTxt("ntm:library", "%s failed (%d): %s", what, rc, g_ctx ? ntm_last_error(g_ctx) : "no context");
+    }
+}
+
+static ntm_ctx* ctx(void) {
+    if (!g_ctx) {
+        check(ntm_ctx_create(&g_ctx, 0), "ntm_ctx_create");
+        mexAtExit(release);
+    }
+    return g_ctx;
+}
+
+static double scalar_field(const mxArray* s, const char* name, double dflt) {
+    const mxArray* f = s ? mxGetField(s, 0, name) : NULL;
+    return (f && mxIsDouble(f) && mxGetNumberOfElements(f) >= 1) ? mxGetDoubles(f)[0] : dflt;
+}
+
+static void vec_field(const mxArray* s, const char* name, double* dst, size_t n) {
+    const mxArray* f = s ? mxGetField(s, 0, name) : NULL;
+    if (!f) return;
+    if (!mxIsDouble(f) || mxGetNumberOfElements(f) != n) mexErrMsgIdAndTxt("ntm:cfg", "cfg.%s must have %d doubles", name, (int)n);
+    memcpy(dst, mxGetDoubles(f), n * sizeof(double));
+}
+
+static ntm_config read_cfg(const mxArray* s) {
+    ntm_config c;
+    if (s && !mxIsStruct(s)) mexErrMsgIdAndTxt("ntm:cfg", "cfg must be a struct");
+    ntm_config_default(&c, (int32_t)scalar_field(s, "N", 20));
+    c.i_sim = (int32_t)scalar_field(s, "i_sim", c.i_sim);
+    c.mode = (int32_t)scalar_field(s, "mode", c.mode);
+    c.flags = (int32_t)scalar_field(s, "flags", c.flags);
+    c.Ts = scalar_field(s, "Ts", c.Ts);
+    c.umin = scalar_field(s, "umin", c.umin);
+    c.umax = scalar_field(s, "umax", c.umax);
+    c.epsilon = scalar_field(s, "epsilon", c.epsilon);
+    vec_field(s, "xmin", c.xmin, 2);
+    vec_field(s, "xmax", c.xmax, 2);
+    vec_field(s, "r", c.r, 2);
+    if (s && mxGetField(s, 0, "Q")) {   /* MATLAB 2x2 is column-major; the ABI's Q is row-major */
+        double q[4];
+        vec_field(s, "Q", q, 4);
+        c.Q[0] = q[0]; c.Q[1] = q[2]; c.Q[2] = q[1]; c.Q[3] = q[3];
+    }
+    return c;
+}
+
+static const double* in_matrix(const mxArray* a, size_t rows, size_t cols, const char* name) {
+    if (!mxIsDouble(a) || mxIsComplex(a) || mxGetM(a) != rows || mxGetN(a) != cols)
+        mexErrMsgIdAndTxt("ntm:arg", "%s must be a real %d-by-%d double array", name, (int)rows, (int)cols);
+    return mxGetDoubles(a);
+}
+
+static void do_step(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    if (nrhs < 4) mexErrMsgIdAndTxt("ntm:arg", "usage: ntm_mpc_mex('step', x_k, rho, Uold[, cfg])");
+    const ntm_config c = read_cfg(nrhs > 4 ? prhs[4] : NULL);
+    ntm_physics p;
+    ntm_physics_default(&p);
+    const size_t B = mxGetM(prhs[1]), N = (size_t)c.N;
+    const double* x = in_matrix(prhs[1], B, 2, "x_k");
+    in_matrix(prhs[2], B, 3 * N, "rho");
+    in_matrix(prhs[3], B, N, "Uold");
+    /* value semantics: rho / Uold are updated in copies returned as outputs 6-7 */
+    mxArray* rho = mxDuplicateArray(prhs[2]);
+    mxArray* uold = mxDuplicateArray(prhs[3]);
+    mxArray* U = mxCreateDoubleMatrix(B, N, mxREAL);
+    mxArray* xp = mxCreateDoubleMatrix(B, 2 * (N + 1), mxREAL);
+    mxArray* xn = mxCreateDoubleMatrix(B, 2, mxREAL);
+    mxArray* fl = mxCreateNumericMatrix(B, 1, mxINT32_CLASS, mxREAL);
+    mxArray* it = mxCreateNumericMatrix(B, 1, mxINT32_CLASS, mxREAL);
+    check(ntm_mpc_step(ctx(), &p, &c, (int64_t)B, x, mxGetDoubles(rho), mxGetDoubles(uold), mxGetDoubles(U),
+                       mxGetDoubles(xp), mxGetDoubles(xn), mxGetInt32s(fl), mxGetInt32s(it)),
+          "ntm_mpc_step");
+    mxArray* outs[7] = {U, xp, xn, fl, it, rho, uold};
+    for (int i = 0; i < 7; ++i) {
+        if (i < (nlhs > 0 ? nlhs : 1)) plhs[i] = outs[i];
+        else mxDestroyArray(outs[i]);
+    }
+}
+
+static void do_init(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    if (nrhs < 2) mexErrMsgIdAndTxt("ntm:arg", "usage: ntm_mpc_mex('init', x0[, cfg])");
+    const ntm_config c = read_cfg(nrhs > 2 ? prhs[2] : NULL);
+    ntm_physics p;
+    ntm_physics_default(&p);
+    const size_t B = mxGetM(prhs[1]), N = (size_t)c.N;
+    const double* x0 = in_matrix(prhs[1], B, 2, "x0");
+    mxArray* rho = mxCreateDoubleMatrix(B, 3 * N, mxREAL);
+    mxArray* uold = mxCreateDoubleMatrix(B, N, mxREAL);
+    check(ntm_mpc_init(ctx(), &p, &c, (int64_t)B, x0, mxGetDoubles(rho), mxGetDoubles(uold)), "ntm_mpc_init");
+    plhs[0] = rho;
+    if (nlhs > 1) plhs[1] = uold;
+    else mxDestroyArray(uold);
+}
+
+static void do_run(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    if (nrhs < 3) mexErrMsgIdAndTxt("ntm:arg", "usage: ntm_mpc_mex('run', x0, k_sim[, cfg])");
+    const ntm_config c = read_cfg(nrhs > 3 ? prhs[3] : NULL);
+    ntm_physics p;
+    ntm_physics_default(&p);
+    const size_t B = mxGetM(prhs[1]), N = (size_t)c.N;
+    const double* x0 = in_matrix(prhs[1], B, 2, "x0");
+    const int k = (int)mxGetScalar(prhs[2]);
+    if (k < 1) mexErrMsgIdAndTxt("ntm:arg", "k_sim must be >= 1");
+    mxArray* xk = mxCreateDoubleMatrix(B, 2 * (size_t)(k + 1), mxREAL);
+    mxArray* uk = mxCreateDoubleMatrix(B, (size_t)k, mxREAL);
+    mxArray* Uk = mxCreateDoubleMatrix(B, N * (size_t)k, mxREAL);
+    mxArray* wp = mxCreateDoubleMatrix(B, (N + 1) * (size_t)k, mxREAL);
+    mxArray* fl = mxCreateNumericMatrix(B, (size_t)k, mxINT32_CLASS, mxREAL);
+    mxArray* it = mxCreateNumericMatrix(B, (size_t)k, mxINT32_CLASS, mxREAL);
+    check(ntm_mpc_run(ctx(), &p, &c, (int64_t)B, k, x0, mxGetDoubles(xk), mxGetDoubles(uk), mxGetDoubles(Uk),
+                      mxGetDoubles(wp), mxGetInt32s(fl), mxGetInt32s(it)),
+          "ntm_mpc_run");
+    mxArray* outs[6] = {xk, uk, Uk, wp, fl, it};
+    for (int i = 0; i < 6; ++i) {
+        if (i < (nlhs > 0 ? nlhs : 1)) plhs[i] = outs[i];
+        else mxDestroyArray(outs[i]);
+    }
+}
+
+void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+    if (nrhs < 1 || !mxIsChar(prhs[0]))
+        mexErrMsgIdAndTxt("ntm:arg", "first argument: 'init', 'step', 'run' or 'close'");
+    char cmd[16];
+    mxGetString(prhs[0], cmd, sizeof cmd);
+    if (!strcmp(cmd, "step")) do_step(nlhs, plhs, nrhs, prhs);
+    else if (!strcmp(cmd, "init")) do_init(nlhs, plhs, nrhs, prhs);
+    else if (!strcmp(cmd, "run")) do_run(nlhs, plhs, nrhs, prhs);
+    else if (!strcmp(cmd, "close")) release();
+    else mexErrMsgIdAndTxt("ntm:arg", "unknown command '%s'", cmd);
+}

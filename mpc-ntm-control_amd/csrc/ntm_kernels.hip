@@ -170,6 +170,20 @@ __global__ void k_rho(Prob pb, int64_t B, const double* x, double* rho) {
     rho[2 * B + s] = r3;
 }
 
+// initial LPV state: Rho = repmat(rho(x0), 1, N) (NTM_MPC_Sim.m:63-65), Uold = +Inf (D14)
+__global__ void k_init_state(Prob pb, int64_t B, const double* x, double* rho, double* U_old) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= B) return;
+    double r1, r2, r3;
+    rho_eval(pb.k, x[s], x[B + s], r1, r2, r3);
+    for (int i = 0; i < pb.N; ++i) {
+        rho[(int64_t)(3 * i) * B + s] = r1;
+        rho[(int64_t)(3 * i + 1) * B + s] = r2;
+        rho[(int64_t)(3 * i + 2) * B + s] = r3;
+        U_old[(int64_t)i * B + s] = __builtin_inf();
+    }
+}
+
 __global__ void k_AB(Prob pb, int64_t B, const double* rho, double* A, double* Bv) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= B) return;
@@ -706,6 +720,37 @@ int ntm_rho_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg,
     Prob pb = make_prob(phys, cfg);
     hipLaunchKernelGGL(k_rho, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, (hipStream_t)stream, pb, B, x, rho);
     return check_hip(ctx, hipGetLastError(), "k_rho");
+}
+
+int ntm_mpc_init_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* x0,
+                        double* rho, double* U_old, void* stream) {
+    int rc = validate(ctx, phys, cfg, B);
+    if (rc || B == 0) return rc;
+    if (!x0 || !rho || !U_old) return fail(ctx, NTM_E_INVALID, "null array");
+    Prob pb = make_prob(phys, cfg);
+    hipLaunchKernelGGL(k_init_state, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, (hipStream_t)stream, pb, B,
+                       x0, rho, U_old);
+    return check_hip(ctx, hipGetLastError(), "k_init_state");
+}
+
+int ntm_mpc_init(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* x0,
+                 double* rho, double* U_old) {
+    int rc = validate(ctx, phys, cfg, B);
+    if (rc || B == 0) return rc;
+    if (!x0 || !rho || !U_old) return fail(ctx, NTM_E_INVALID, "null array");
+    const int N = cfg->N;
+    size_t bx = al(2 * B * 8), brho = al(3 * N * B * 8), bu = al(N * B * 8);
+    if ((rc = ensure_buf(ctx, bx + brho + bu))) return rc;
+    char* p = static_cast<char*>(ctx->dbuf);
+    double* dx = (double*)p; p += bx;
+    double* drho = (double*)p; p += brho;
+    double* duo = (double*)p;
+    hipStream_t st = ctx->stream;
+    if ((rc = check_hip(ctx, hipMemcpyAsync(dx, x0, 2 * B * 8, hipMemcpyHostToDevice, st), "H2D"))) return rc;
+    if ((rc = ntm_mpc_init_device(ctx, phys, cfg, B, dx, drho, duo, st))) return rc;
+    if ((rc = check_hip(ctx, hipMemcpyAsync(rho, drho, 3 * N * B * 8, hipMemcpyDeviceToHost, st), "D2H"))) return rc;
+    if ((rc = check_hip(ctx, hipMemcpyAsync(U_old, duo, N * B * 8, hipMemcpyDeviceToHost, st), "D2H"))) return rc;
+    return check_hip(ctx, hipStreamSynchronize(st), "sync");
 }
 
 int ntm_AB_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* rho,

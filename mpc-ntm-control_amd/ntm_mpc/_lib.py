@@ -56,6 +56,8 @@ EXPORTS = {
     "ntm_ctx_set_stats": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ntm_debug_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "ntm_step_launch_info": (C.c_int, [C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "ntm_mpc_init": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _DP, _DP, _DP]),
+    "ntm_mpc_init_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _V, _V, _V, _V]),
     "ntm_mpc_step": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _DP, _DP, _DP, _DP, _DP, _DP, _IP, _IP]),
     "ntm_mpc_step_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
     "ntm_mpc_run": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, C.c_int32, _DP, _DP, _DP, _DP, _DP, _IP, _IP]),

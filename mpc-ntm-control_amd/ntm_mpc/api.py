@@ -26,6 +26,7 @@ import ctypes as C
 import math
 from dataclasses import dataclass, field
 
+import numpy as np
 import torch
 
 from . import _lib as L
@@ -168,9 +169,23 @@ class NtmMpc:
         """Rho = repmat(rho(x0), 1, N) (NTM_MPC_Sim.m:63-65); U_old = +inf (D14)."""
         cfg = cfg or self.config
         Bn = x0.shape[1]
-        r = self.rho(x0, cfg)                                   # (3, B)
-        rho = r.repeat(cfg.N, 1).contiguous()                   # (3N, B): element 3i + k
-        U_old = torch.full((cfg.N, Bn), float("inf"), dtype=torch.float64, device=x0.device)
+        _check_dev(x0, (2, Bn), name="x0")
+        rho, U_old = self._empty(3 * cfg.N, Bn), self._empty(cfg.N, Bn)
+        self._raise(self.lib.ntm_mpc_init_device(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn,
+                                                 _ptr(x0), _ptr(rho), _ptr(U_old), self._stream()),
+                    "ntm_mpc_init_device")
+        return rho, U_old
+
+    def initial_state_host(self, x0: np.ndarray, cfg: Config | None = None):
+        """ntm_mpc_init with host arrays (the MEX path)."""
+        cfg = cfg or self.config
+        Bn = x0.shape[1]
+        if x0.shape != (2, Bn) or x0.dtype != np.float64 or not x0.flags.c_contiguous:
+            raise ValueError("x0: expected C-contiguous float64 (2, B)")
+        rho, U_old = np.empty((3 * cfg.N, Bn)), np.empty((cfg.N, Bn))
+        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))          # noqa: E731
+        self._raise(self.lib.ntm_mpc_init(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn,
+                                          dp(x0), dp(rho), dp(U_old)), "ntm_mpc_init")
         return rho, U_old
 
     def step(self, x_k: torch.Tensor, rho: torch.Tensor, U_old: torch.Tensor, cfg: Config | None = None,
@@ -208,6 +223,43 @@ class NtmMpc:
                                          _ptr(out["wpred"]), _ptr(out["exitflag"]), _ptr(out["inner_iters"]),
                                          self._stream())
         self._raise(rc, "ntm_mpc_run_device")
+        return out
+
+    # ------------------------------------------------------------ host-buffer entry points (the MEX path)
+    def step_host(self, x_k: np.ndarray, rho: np.ndarray, U_old: np.ndarray, cfg: Config | None = None):
+        """ntm_mpc_step with host (NumPy, C-contiguous fp64) arrays, as a MEX
+        gateway calls it: the library stages through its own device buffers.
+        ``rho`` and ``U_old`` are updated in place."""
+        cfg = cfg or self.config
+        N, Bn = cfg.N, x_k.shape[1]
+        for a, shp, nm in ((x_k, (2, Bn), "x_k"), (rho, (3 * N, Bn), "rho"), (U_old, (N, Bn), "U_old")):
+            if a.shape != shp or a.dtype != np.float64 or not a.flags.c_contiguous:
+                raise ValueError(f"{nm}: expected C-contiguous float64 {shp}")
+        out = {"U": np.empty((N, Bn)), "x_pred": np.empty((2 * (N + 1), Bn)), "x_next": np.empty((2, Bn)),
+               "exitflag": np.empty(Bn, np.int32), "inner_iters": np.empty(Bn, np.int32)}
+        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))          # noqa: E731
+        ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))           # noqa: E731
+        rc = self.lib.ntm_mpc_step(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn, dp(x_k),
+                                   dp(rho), dp(U_old), dp(out["U"]), dp(out["x_pred"]), dp(out["x_next"]),
+                                   ip(out["exitflag"]), ip(out["inner_iters"]))
+        self._raise(rc, "ntm_mpc_step")
+        return out
+
+    def run_host(self, x0: np.ndarray, k_sim: int = 20, cfg: Config | None = None):
+        """ntm_mpc_run with host arrays (NTM_MPC_Sim.m:80-131 for a batch)."""
+        cfg = cfg or self.config
+        N, Bn = cfg.N, x0.shape[1]
+        if x0.shape != (2, Bn) or x0.dtype != np.float64 or not x0.flags.c_contiguous:
+            raise ValueError("x0: expected C-contiguous float64 (2, B)")
+        out = {"xk": np.empty((2 * (k_sim + 1), Bn)), "uk": np.empty((k_sim, Bn)), "Uk": np.empty((N * k_sim, Bn)),
+               "wpred": np.empty(((N + 1) * k_sim, Bn)), "exitflag": np.empty((k_sim, Bn), np.int32),
+               "inner_iters": np.empty((k_sim, Bn), np.int32)}
+        dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))          # noqa: E731
+        ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))           # noqa: E731
+        rc = self.lib.ntm_mpc_run(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn, k_sim, dp(x0),
+                                  dp(out["xk"]), dp(out["uk"]), dp(out["Uk"]), dp(out["wpred"]),
+                                  ip(out["exitflag"]), ip(out["inner_iters"]))
+        self._raise(rc, "ntm_mpc_run")
         return out
 
     # ------------------------------------------------------------ function level

@@ -263,3 +263,30 @@ def test_step_matches_run_first_step(ctl):
     rn = ctl.run(T(x0), 1, cfg)
     assert torch.equal(st["U"][0], rn["uk"][0])
     assert torch.equal(st["x_next"], rn["xk"][2:4])
+
+
+@pytest.mark.gpu
+def test_host_buffer_entry_points_match_device(ctl):
+    """ntm_mpc_step / ntm_mpc_run with host arrays (the MEX boundary) give
+    bit-identical results to the device-pointer entry points."""
+    N, B = 20, 40
+    cfg, ocfg = cfgs(N, 2)
+    x0 = np.ascontiguousarray(O.scenario_x0(np.arange(B)).T)
+    rho, Uo = ctl.initial_state(T(x0), cfg)
+    rho_h, uo_h = ctl.initial_state_host(x0, cfg)
+    np.testing.assert_array_equal(rho_h, H(rho))
+    assert np.all(np.isinf(uo_h)) and np.all(uo_h > 0)
+    r_or, u_or = cbind.initial_state(x0, ocfg)
+    np.testing.assert_allclose(rho_h, r_or, rtol=1e-15)
+    for _ in range(3):
+        dv = ctl.step(T(x0), rho, Uo, cfg)
+        hs = ctl.step_host(x0, rho_h, uo_h, cfg)
+        for k in ("U", "x_pred", "x_next", "exitflag", "inner_iters"):
+            np.testing.assert_array_equal(hs[k], H(dv[k]), err_msg=k)
+        np.testing.assert_array_equal(rho_h, H(rho))
+        np.testing.assert_array_equal(uo_h, H(Uo))
+        x0 = np.ascontiguousarray(hs["x_next"])
+    rd = ctl.run(T(x0), 3, cfg)
+    rh = ctl.run_host(x0, 3, cfg)
+    for k in rd:
+        np.testing.assert_array_equal(rh[k], H(rd[k]), err_msg=k)
