@@ -99,10 +99,11 @@ def main():
     # shard: global scenario ids [rank*B, (rank+1)*B)  (shard-invariant inputs)
     x = torch.tensor(ntm_mpc.scenarios_x0(rank * B, B), device=dev)
     rho, U_old = ctl.initial_state(x, cfg)
+    active_ws = ctl.new_active_ws(B, cfg)       # last two active sets, carried step to step
     outs = [None, None]
 
     def one_step(i, xin):
-        out = ctl.step(xin, rho, U_old, cfg, out=outs[i & 1])
+        out = ctl.step(xin, rho, U_old, cfg, out=outs[i & 1], active_ws=active_ws)
         outs[i & 1] = out
         return out
 
@@ -111,15 +112,15 @@ def main():
         x = one_step(i, x)["x_next"].clone()
     # instrumentation pass (untimed, separate launch on a copy of the state)
     stats = torch.zeros(STATS_ROWS, B, dtype=torch.int32, device=dev)
-    rho_s, uo_s = rho.clone(), U_old.clone()
+    rho_s, uo_s, ws_s = rho.clone(), U_old.clone(), active_ws.clone()
     ctl.set_stats(stats)
-    ctl.step(x, rho_s, uo_s, cfg)
+    ctl.step(x, rho_s, uo_s, cfg, active_ws=ws_s)
     ctl.set_stats(None)
     torch.cuda.synchronize()
     st = stats.double().sum(dim=1).cpu().numpy()
     qps, Kgi, tries, giruns = st[0] / B, st[1] / B, st[4] / B, st[5] / B     # per MPC step
     qact, sgen = st[2] / st[0], st[3] / st[0]                                 # per QP
-    del rho_s, uo_s
+    del rho_s, uo_s, ws_s
 
     hist_u = torch.empty(K, B, dtype=torch.float64, device=dev)
     hist_x = torch.empty(K, 2, B, dtype=torch.float64, device=dev)

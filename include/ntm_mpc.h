@@ -123,6 +123,23 @@ int ntm_mpc_step_device(ntm_ctx* ctx, const ntm_physics* phys,
                         double* x_next, int32_t* exitflag, int32_t* inner_iters,
                         void* stream);
 
+/* Same, with an optional warm-start workspace carried from step to step:
+ * active_ws[2(N+1)] int32 per scenario (in/out; initialise every entry to -1;
+ * NULL = none) holds the active sets of the previous step's last two QPs.
+ * They are tried first and taken only when the exact re-solve passes the KKT
+ * certificate, so the result is the QP optimum either way;
+ * entries that are not a valid active set are ignored.  ntm_mpc_run keeps
+ * this state on chip by itself. */
+int ntm_mpc_step_ws(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg,
+                    int64_t B, const double* x_k, double* rho, double* U_old,
+                    double* U, double* x_pred, double* x_next,
+                    int32_t* exitflag, int32_t* inner_iters, int32_t* active_ws);
+int ntm_mpc_step_ws_device(ntm_ctx* ctx, const ntm_physics* phys,
+                           const ntm_config* cfg, int64_t B, const double* x_k,
+                           double* rho, double* U_old, double* U, double* x_pred,
+                           double* x_next, int32_t* exitflag, int32_t* inner_iters,
+                           int32_t* active_ws, void* stream);
+
 /* Closed loop NTM_MPC_Sim.m:80-131 over k_sim steps, device-resident.
  * x0[2]; outputs xk[2(k_sim+1)] (2x(k_sim+1)), uk[k_sim], Uk[N k_sim]
  * (N x k_sim), wpred[(N+1) k_sim] (predicted island width per step),

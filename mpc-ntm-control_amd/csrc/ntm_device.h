@@ -569,6 +569,10 @@ struct Pick {
     double bc;    // normalised GI right-hand side
 };
 
+// aflag bits per constraint row
+constexpr unsigned char kActiveRow = 1;   // in GI's active set
+constexpr unsigned char kCandRow = 2;     // row of a failed warm-start candidate (GI adds these first)
+
 // Implicit getWLc rows: u-bounds are -+e_j, state rows are -+Gamma_r; the
 // rows are never materialised.
 struct StructRows {
@@ -657,6 +661,10 @@ struct StructRows {
 
     // Most violated inactive row (verify = false), or, with verify = true,
     // whether EVERY row has slack >= -tol * max(vmax, |bc|) (returned in .p).
+    // Rows flagged kCandRow (the rows of a warm-start candidate that failed
+    // its certificate) are taken first while any of them is violated beyond
+    // GI's stopping tolerance: GI may add any violated row, so this only
+    // steers it towards the nearby active set.
     template <int P, class W>
     __device__ Pick check(const W& w, double Vl, int l, bool verify = false, double vmax = 1.0) const {
         const int N = w.n();
@@ -665,7 +673,10 @@ struct StructRows {
         int bid = 0x7fffffff, bad = 0;
         auto consider = [&](double s, int id, double bcv) {
             if (verify) { bad |= s < -1e-9 * fmax(vmax, fabs(bcv)); return; }
-            if (!w.aflag()[id] && (s < bv || (s == bv && id < bid))) { bv = s; bid = id; bs = s; bbc = bcv; }
+            const unsigned char fl = w.aflag()[id];
+            if (fl & kActiveRow) return;
+            const double key = ((fl & kCandRow) && s < -1e-12 * fmax(vmax, fabs(bcv))) ? s - 1e200 : s;
+            if (key < bv || (key == bv && id < bid)) { bv = key; bid = id; bs = s; bbc = bcv; }
         };
         if (l < N) {
             double lo = w.vlo()[l];
@@ -760,7 +771,7 @@ struct DenseRows {
         int bid = 0x7fffffff, bad = 0;
         for (int i = l; i < m; i += P) {
             double rn = rnrm[i];
-            if (rn > 0.0 && (verify || !w.aflag()[i])) {
+            if (rn > 0.0 && (verify || !(w.aflag()[i] & kActiveRow))) {
                 double sl = 0.0;
                 for (int j = 0; j < w.n(); ++j) sl -= ((lin(w, i, j) * w.D()[j]) / rn) * w.V()[j];
                 double bi = bval(w, i) / rn;
@@ -892,8 +903,8 @@ __device__ int gi_solve(const W& w, const Rows* rows, int nrows, int l, int* ite
     const int max_iter = 10 * (N + nrows) + 50;
     int q = 0, it = 0;
     for (;;) {
-        Pick pk = rows->template check<P>(w, Vl, l);
-        double vmax = gmax<P>(l < N ? fabs(Vl) : 0.0);
+        const double vmax = gmax<P>(l < N ? fabs(Vl) : 0.0);
+        Pick pk = rows->template check<P>(w, Vl, l, false, fmax(1.0, vmax));
         NTM_ACC(ST_GI_CHECK, tg);
         NTM_CNT(CN_CHECK);
         if (pk.p < 0 || pk.s >= -1e-12 * fmax(fmax(1.0, vmax), fabs(pk.bc))) {
@@ -979,7 +990,7 @@ __device__ int gi_solve(const W& w, const Rows* rows, int nrows, int l, int* ite
                         w.R()[q + q * LD] = h;
                         w.T()[q * LDJ + q] = ih;
                         w.act()[q] = p;
-                        w.aflag()[p] = 1;
+                        w.aflag()[p] = kActiveRow;
                         w.uu()[q] = upq;
                     }
                     ++q;
@@ -1307,12 +1318,15 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
             w.srw()[k] = srow;
             w.ssg()[k] = ssign;
         } else {
-            w.fx()[fixj] = 1;
+            w.fx()[fixj] = (unsigned char)(l + 1);       // tagged by the writing lane
             w.Uf()[fixj] = ufix;
             w.hv()[fixj] = nfix;
         }
     }
     NTM_WSYNC();
+    // two active rows fixing one variable (only a caller-supplied candidate can
+    // do that; GI never adds a dependent row) cannot be certified: reject
+    const bool collide = gmaxi<P>((l < q && !isgen && w.fx()[fixj] != (unsigned char)(l + 1)) ? 1 : 0) != 0;
     const bool fixed = (l < N) && w.fx()[l];
     const double uf = fixed ? w.Uf()[l] : 0.0;
     const double vb = fixed ? uf / w.D()[l] : 0.0;
@@ -1361,7 +1375,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
         const int r = w.srw()[s2];
         return (j <= (r >> 1)) ? -(((w.ssg()[s2] * w.gt(r, j)) * w.D()[j]) * w.irn()[r]) : 0.0;
     };
-    bool ok = chol_inplace<P>(w.R(), nF, 1, LD, l, w.ldi());
+    bool ok = !collide && chol_inplace<P>(w.R(), nF, 1, LD, l, w.ldi());
     double vfin = 0.0;
     if (ok) {
         const double wl = fwd_lanes<P>(w.R(), w.ldi(), nF, 1, LD, gl, l);    // L^{-1} g_F
@@ -1569,6 +1583,9 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                     q = cq;
                     done = true;
                     NTM_CNT(CN_HIT);
+                } else {
+                    if (l < cq) w.aflag()[cand[l]] = kCandRow;
+                    NTM_WSYNC();
                 }
                 NTM_ACC(ST_CAND, tq);
             }

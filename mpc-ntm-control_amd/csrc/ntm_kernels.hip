@@ -46,6 +46,41 @@ __device__ __forceinline__ int64_t xcd_swizzle(int64_t b, int64_t nb) {
     return x * q + (x < r ? x : r) + k;
 }
 
+// Warm-start workspace (ntm_mpc_step_ws): the active sets of the previous
+// step's last two QPs, 2 slots x (N ids + count) per scenario, in/out.  It is
+// only a hint (every candidate is re-solved exactly and KKT-certified), but it
+// comes from the caller, so each slot is validated before use: count in
+// [0, N], ids in [0, rows), no repeats; anything else disables the slot.
+template <int P, class W>
+__device__ void load_candidates(const Prob& pb, const W& w, int64_t B, int64_t s, const int32_t* ws, int l) {
+    const int N = w.n();
+    const int nrows = pb.mode == NTM_MODE_BOX ? 2 * N : (pb.mode == NTM_MODE_FULL ? 6 * N + 4 : 0);
+    for (int e = l; e < 2 * (N + 1); e += P) w.cand()[e] = ws[(int64_t)e * B + s];
+    for (int i = l; i < nrows; i += P) w.aflag()[i] = 0;
+    NTM_WSYNC();
+    for (int slot = 0; slot < 2; ++slot) {
+        int* c = w.cand() + slot * (N + 1);
+        const int q = uni<P>(c[N]);
+        if (q < 0) continue;
+        bool bad = q > N || nrows == 0;
+        if (!bad) {
+            int lb = 0;
+            if (l < q) lb = (c[l] < 0 || c[l] >= nrows) ? 1 : 0;
+            bad = gmaxi<P>(lb) != 0;
+        }
+        if (!bad) {
+            int lb = 0;
+            for (int i = 0; i < q; ++i) {         // lane l < q checks its id against the earlier ones
+                const int ci = c[i];
+                if (l < q && i < l && ci == c[l]) lb = 1;
+            }
+            bad = gmaxi<P>(lb) != 0;
+        }
+        if (bad && l == 0) c[N] = -1;
+        NTM_WSYNC();
+    }
+}
+
 // one MPC step on LDS-resident state; returns exit flag, sets *iters
 template <int P, class W>
 __device__ int mpc_step_dev(const Prob& pb, const W& w, double x0, double x1, int l, int* iters,
@@ -84,7 +119,7 @@ __global__ __launch_bounds__(64, NTM_HOT_WAVES_PER_EU) void k_mpc_step(Prob pb, 
                                                  double* __restrict__ rho, double* __restrict__ U_old,
                                                  double* __restrict__ U, double* __restrict__ x_pred,
                                                  double* __restrict__ x_next, int32_t* __restrict__ exitflag,
-                                                 int32_t* __restrict__ inner_iters) {
+                                                 int32_t* __restrict__ inner_iters, int32_t* __restrict__ active_ws) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int G = 64 / P;
     const int g = threadIdx.x / P, l = threadIdx.x % P;
@@ -94,7 +129,8 @@ __global__ __launch_bounds__(64, NTM_HOT_WAVES_PER_EU) void k_mpc_step(Prob pb, 
     if (s >= B) return;
     auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
     const double x0 = x_k[s], x1 = x_k[B + s];
-    if (l < 2) w.cand()[l * (N + 1) + N] = -1;
+    if (active_ws) load_candidates<P>(pb, w, B, s, active_ws, l);
+    else if (l < 2) w.cand()[l * (N + 1) + N] = -1;
     load_state<P>(w, B, s, rho, U_old, l);
     int its;
     int flag = mpc_step_dev<P>(pb, w, x0, x1, l, &its, B, s);
@@ -112,6 +148,8 @@ __global__ __launch_bounds__(64, NTM_HOT_WAVES_PER_EU) void k_mpc_step(Prob pb, 
         exitflag[s] = flag;
         inner_iters[s] = its;
     }
+    if (active_ws)
+        for (int e = l; e < 2 * (N + 1); e += P) active_ws[(int64_t)e * B + s] = w.cand()[e];
     NTM_STAMPS_FLUSH();
 }
 
@@ -441,7 +479,7 @@ int set_lds(ntm_ctx* ctx, K kern, size_t lds) {
 template <int P, int NN>
 int launch_step(ntm_ctx* ctx, const Prob& pb, int64_t B, const double* x_k, double* rho, double* U_old,
                 double* U, double* x_pred, double* x_next, int32_t* exitflag, int32_t* inner_iters,
-                hipStream_t st) {
+                int32_t* active_ws, hipStream_t st) {
     constexpr int G = 64 / P;
     size_t lds = (size_t)G * ws_bytes(pb.N);
     int rc = set_lds(ctx, k_mpc_step<P, NN>, lds);
@@ -449,7 +487,7 @@ int launch_step(ntm_ctx* ctx, const Prob& pb, int64_t B, const double* x_k, doub
     int64_t blocks = (B + G - 1) / G;
     if (blocks == 0) return NTM_OK;
     hipLaunchKernelGGL((k_mpc_step<P, NN>), dim3((unsigned)blocks), dim3(64), lds, st, pb, B, x_k, rho, U_old, U,
-                       x_pred, x_next, exitflag, inner_iters);
+                       x_pred, x_next, exitflag, inner_iters, active_ws);
     return check_hip(ctx, hipGetLastError(), "k_mpc_step launch");
 }
 
@@ -601,6 +639,13 @@ int ntm_ctx_set_stats(ntm_ctx* ctx, int32_t* dev_stats) {
 int ntm_mpc_step_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B,
                         const double* x_k, double* rho, double* U_old, double* U, double* x_pred, double* x_next,
                         int32_t* exitflag, int32_t* inner_iters, void* stream) {
+    return ntm_mpc_step_ws_device(ctx, phys, cfg, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters,
+                                  nullptr, stream);
+}
+
+int ntm_mpc_step_ws_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B,
+                           const double* x_k, double* rho, double* U_old, double* U, double* x_pred, double* x_next,
+                           int32_t* exitflag, int32_t* inner_iters, int32_t* active_ws, void* stream) {
     int rc = validate(ctx, phys, cfg, B);
     if (rc) return rc;
     if (B == 0) return NTM_OK;
@@ -609,7 +654,8 @@ int ntm_mpc_step_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config*
     Prob pb = make_prob(phys, cfg);
     pb.stats = ctx->stats;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-#define CALL(P, NN) launch_step<P, NN>(ctx, pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, st)
+#define CALL(P, NN) \
+    launch_step<P, NN>(ctx, pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, active_ws, st)
     return NTM_DISPATCH_P(cfg->N, CALL);
 #undef CALL
 }
@@ -624,6 +670,12 @@ int ntm_step_launch_info(int32_t N, int32_t* lanes, int32_t* horizon_template) {
 int ntm_mpc_step(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* x_k,
                  double* rho, double* U_old, double* U, double* x_pred, double* x_next, int32_t* exitflag,
                  int32_t* inner_iters) {
+    return ntm_mpc_step_ws(ctx, phys, cfg, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, nullptr);
+}
+
+int ntm_mpc_step_ws(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* x_k,
+                    double* rho, double* U_old, double* U, double* x_pred, double* x_next, int32_t* exitflag,
+                    int32_t* inner_iters, int32_t* active_ws) {
     int rc = validate(ctx, phys, cfg, B);
     if (rc) return rc;
     if (B == 0) return NTM_OK;
@@ -631,8 +683,8 @@ int ntm_mpc_step(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, i
         return fail(ctx, NTM_E_INVALID, "null array");
     const int N = cfg->N;
     size_t bx = al(2 * B * 8), brho = al(3 * N * B * 8), bu = al(N * B * 8), bxp = al(2 * (N + 1) * B * 8),
-           bi = al(B * 4);
-    rc = ensure_buf(ctx, bx * 2 + brho + bu * 2 + bxp + bi * 2);
+           bi = al(B * 4), bws = active_ws ? al(2 * (N + 1) * B * 4) : 0;
+    rc = ensure_buf(ctx, bx * 2 + brho + bu * 2 + bxp + bi * 2 + bws);
     if (rc) return rc;
     char* p = static_cast<char*>(ctx->dbuf);
     double* dx = (double*)p; p += bx;
@@ -642,12 +694,16 @@ int ntm_mpc_step(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, i
     double* dxp = (double*)p; p += bxp;
     double* dxn = (double*)p; p += bx;
     int32_t* dfl = (int32_t*)p; p += bi;
-    int32_t* dit = (int32_t*)p;
+    int32_t* dit = (int32_t*)p; p += bi;
+    int32_t* dws = active_ws ? (int32_t*)p : nullptr;
     hipStream_t st = ctx->stream;
+    const size_t wsb = 2 * (size_t)(N + 1) * B * 4;
     if ((rc = check_hip(ctx, hipMemcpyAsync(dx, x_k, 2 * B * 8, hipMemcpyHostToDevice, st), "H2D"))) return rc;
     if ((rc = check_hip(ctx, hipMemcpyAsync(drho, rho, 3 * N * B * 8, hipMemcpyHostToDevice, st), "H2D"))) return rc;
     if ((rc = check_hip(ctx, hipMemcpyAsync(duo, U_old, N * B * 8, hipMemcpyHostToDevice, st), "H2D"))) return rc;
-    rc = ntm_mpc_step_device(ctx, phys, cfg, B, dx, drho, duo, dU, dxp, dxn, dfl, dit, st);
+    if (dws && (rc = check_hip(ctx, hipMemcpyAsync(dws, active_ws, wsb, hipMemcpyHostToDevice, st), "H2D")))
+        return rc;
+    rc = ntm_mpc_step_ws_device(ctx, phys, cfg, B, dx, drho, duo, dU, dxp, dxn, dfl, dit, dws, st);
     if (rc) return rc;
     if ((rc = check_hip(ctx, hipMemcpyAsync(rho, drho, 3 * N * B * 8, hipMemcpyDeviceToHost, st), "D2H"))) return rc;
     if ((rc = check_hip(ctx, hipMemcpyAsync(U_old, duo, N * B * 8, hipMemcpyDeviceToHost, st), "D2H"))) return rc;
@@ -657,6 +713,8 @@ int ntm_mpc_step(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, i
     if ((rc = check_hip(ctx, hipMemcpyAsync(x_next, dxn, 2 * B * 8, hipMemcpyDeviceToHost, st), "D2H"))) return rc;
     if ((rc = check_hip(ctx, hipMemcpyAsync(exitflag, dfl, B * 4, hipMemcpyDeviceToHost, st), "D2H"))) return rc;
     if ((rc = check_hip(ctx, hipMemcpyAsync(inner_iters, dit, B * 4, hipMemcpyDeviceToHost, st), "D2H"))) return rc;
+    if (dws && (rc = check_hip(ctx, hipMemcpyAsync(active_ws, dws, wsb, hipMemcpyDeviceToHost, st), "D2H")))
+        return rc;
     return check_hip(ctx, hipStreamSynchronize(st), "sync");
 }
 

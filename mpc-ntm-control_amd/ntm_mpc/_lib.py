@@ -60,6 +60,9 @@ EXPORTS = {
     "ntm_mpc_init_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _V, _V, _V, _V]),
     "ntm_mpc_step": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _DP, _DP, _DP, _DP, _DP, _DP, _IP, _IP]),
     "ntm_mpc_step_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
+    "ntm_mpc_step_ws": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _DP, _DP, _DP, _DP, _DP, _DP, _IP, _IP, _IP]),
+    "ntm_mpc_step_ws_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _V, _V, _V, _V, _V, _V, _V, _V, _V,
+                                         _V]),
     "ntm_mpc_run": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, C.c_int32, _DP, _DP, _DP, _DP, _DP, _IP, _IP]),
     "ntm_mpc_run_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, C.c_int32, _V, _V, _V, _V, _V, _V,
                                      _V, _V]),

@@ -188,10 +188,17 @@ class NtmMpc:
                                           dp(x0), dp(rho), dp(U_old)), "ntm_mpc_init")
         return rho, U_old
 
+    def new_active_ws(self, B: int, cfg: Config | None = None) -> torch.Tensor:
+        """Empty warm-start workspace for step(..., active_ws=): (2(N+1), B) int32 of -1."""
+        cfg = cfg or self.config
+        return torch.full((2 * (cfg.N + 1), B), -1, dtype=torch.int32, device=f"cuda:{self.device}")
+
     def step(self, x_k: torch.Tensor, rho: torch.Tensor, U_old: torch.Tensor, cfg: Config | None = None,
-             out: dict | None = None):
+             out: dict | None = None, active_ws: torch.Tensor | None = None):
         """One MPC time step for a batch (NTM_MPC_Sim.m:94-130).  ``rho`` (3N, B) and
-        ``U_old`` (N, B) are updated in place.  Returns dict U, x_pred, x_next,
+        ``U_old`` (N, B) are updated in place.  ``active_ws`` (see new_active_ws)
+        carries the last two active sets from step to step as verified warm
+        starts (ntm_mpc_step_ws_device).  Returns dict U, x_pred, x_next,
         exitflag, inner_iters (all CUDA tensors)."""
         cfg = cfg or self.config
         N, Bn = cfg.N, x_k.shape[1]
@@ -201,11 +208,13 @@ class NtmMpc:
         if out is None:
             out = {"U": self._empty(N, Bn), "x_pred": self._empty(2 * (N + 1), Bn), "x_next": self._empty(2, Bn),
                    "exitflag": self._empty(Bn, dtype=torch.int32), "inner_iters": self._empty(Bn, dtype=torch.int32)}
-        rc = self.lib.ntm_mpc_step_device(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn,
-                                          _ptr(x_k), _ptr(rho), _ptr(U_old), _ptr(out["U"]), _ptr(out["x_pred"]),
-                                          _ptr(out["x_next"]), _ptr(out["exitflag"]), _ptr(out["inner_iters"]),
-                                          self._stream())
-        self._raise(rc, "ntm_mpc_step_device")
+        if active_ws is not None:
+            _check_dev(active_ws, (2 * (N + 1), Bn), dtype=torch.int32, name="active_ws")
+        rc = self.lib.ntm_mpc_step_ws_device(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn,
+                                             _ptr(x_k), _ptr(rho), _ptr(U_old), _ptr(out["U"]), _ptr(out["x_pred"]),
+                                             _ptr(out["x_next"]), _ptr(out["exitflag"]), _ptr(out["inner_iters"]),
+                                             _ptr(active_ws), self._stream())
+        self._raise(rc, "ntm_mpc_step_ws_device")
         return out
 
     def run(self, x0: torch.Tensor, k_sim: int = 20, cfg: Config | None = None):
@@ -226,7 +235,8 @@ class NtmMpc:
         return out
 
     # ------------------------------------------------------------ host-buffer entry points (the MEX path)
-    def step_host(self, x_k: np.ndarray, rho: np.ndarray, U_old: np.ndarray, cfg: Config | None = None):
+    def step_host(self, x_k: np.ndarray, rho: np.ndarray, U_old: np.ndarray, cfg: Config | None = None,
+                  active_ws: np.ndarray | None = None):
         """ntm_mpc_step with host (NumPy, C-contiguous fp64) arrays, as a MEX
         gateway calls it: the library stages through its own device buffers.
         ``rho`` and ``U_old`` are updated in place."""
@@ -239,10 +249,14 @@ class NtmMpc:
                "exitflag": np.empty(Bn, np.int32), "inner_iters": np.empty(Bn, np.int32)}
         dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))          # noqa: E731
         ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))           # noqa: E731
-        rc = self.lib.ntm_mpc_step(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn, dp(x_k),
-                                   dp(rho), dp(U_old), dp(out["U"]), dp(out["x_pred"]), dp(out["x_next"]),
-                                   ip(out["exitflag"]), ip(out["inner_iters"]))
-        self._raise(rc, "ntm_mpc_step")
+        if active_ws is not None and (active_ws.shape != (2 * (N + 1), Bn) or active_ws.dtype != np.int32
+                                      or not active_ws.flags.c_contiguous):
+            raise ValueError(f"active_ws: expected C-contiguous int32 {(2 * (N + 1), Bn)}")
+        rc = self.lib.ntm_mpc_step_ws(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn, dp(x_k),
+                                      dp(rho), dp(U_old), dp(out["U"]), dp(out["x_pred"]), dp(out["x_next"]),
+                                      ip(out["exitflag"]), ip(out["inner_iters"]),
+                                      None if active_ws is None else ip(active_ws))
+        self._raise(rc, "ntm_mpc_step_ws")
         return out
 
     def run_host(self, x0: np.ndarray, k_sim: int = 20, cfg: Config | None = None):

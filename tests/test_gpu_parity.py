@@ -175,19 +175,24 @@ def test_quadprog_matches_oracle(ctl, mode):
 
 
 # ---------------------------------------------------------------- a7, a12, a13: one MPC step
-@pytest.mark.parametrize("N,mode", [(10, 0), (20, 1), (20, 2), (3, 2), (50, 2), (50, 1)])
-def test_step_teacher_forced(ctl, N, mode):
-    """Each step, the GPU and the oracle get identical (x_k, rho, U_old)."""
+@pytest.mark.parametrize("N,mode,warm", [(10, 0, False), (20, 1, False), (20, 2, False), (3, 2, False),
+                                         (50, 2, False), (50, 1, False), (20, 2, True), (20, 1, True),
+                                         (50, 2, True)])
+def test_step_teacher_forced(ctl, N, mode, warm):
+    """Each step, the GPU and the oracle get identical (x_k, rho, U_old); with
+    warm=True the GPU also carries its active-set workspace from step to step
+    (ntm_mpc_step_ws_device), which must not change the answer."""
     B, k_sim = 48, 12 if N < 50 else 4
     cfg, ocfg = cfgs(N, mode)
     x = O.scenario_x0(np.arange(B)).T if mode else np.tile(O.REFERENCE_X0[:, None], (1, B))
     rho, Uo = cbind.initial_state(x, ocfg)
+    ws = ctl.new_active_ws(B, cfg) if warm else None
     worst, same_iters, n = 0.0, 0, 0
     xscale = np.array([0.15, 2000 * math.pi])[:, None]      # |w|, |omega| magnitudes
     for k in range(k_sim):
         ref = cbind.step(x, rho, Uo, ocfg)
         tr, tu = T(rho), T(Uo)
-        out = ctl.step(T(x), tr, tu, cfg)
+        out = ctl.step(T(x), tr, tu, cfg, active_ws=ws)
         assert (H(out["exitflag"]) == ref["exitflag"]).all(), k
         # the LPV loop stops on sum|U - Uold| < 1e-14 (NTM_MPC_Sim.m:123), i.e. on a
         # bitwise fixed point: GPU and CPU rounding may reach it one iteration apart
@@ -290,3 +295,41 @@ def test_host_buffer_entry_points_match_device(ctl):
     rh = ctl.run_host(x0, 3, cfg)
     for k in rd:
         np.testing.assert_array_equal(rh[k], H(rd[k]), err_msg=k)
+
+
+def test_step_garbage_workspace_is_ignored(ctl):
+    """A caller-supplied warm-start workspace that is not a valid active set
+    (ids out of range, repeats, counts > N) is ignored, never trusted: same
+    flags and the same optimum as with no workspace."""
+    N, B = 20, 64
+    cfg, _ = cfgs(N, 2)
+    x = T(O.scenario_x0(np.arange(B)).T)
+    rng = np.random.default_rng(7)
+    junk = rng.integers(-5, 400, size=(2 * (N + 1), B)).astype(np.int32)
+    junk[N, :B // 2] = rng.integers(-3, 3 * N, size=B // 2)          # counts, many invalid
+    junk[2 * N + 1, :] = N
+    junk[0:4, 10] = 7                                                 # repeats
+    junk[N, 10] = 4
+    rho0, uo0 = ctl.initial_state(x, cfg)
+    ref = ctl.step(x, rho0.clone(), uo0.clone(), cfg)
+    out = ctl.step(x, rho0.clone(), uo0.clone(), cfg, active_ws=T(junk).to(torch.int32))
+    assert torch.equal(out["exitflag"], ref["exitflag"])
+    assert torch.max(torch.abs(out["U"] - ref["U"])).item() <= U_TOL * cfg.umax
+
+
+def test_step_workspace_roundtrip_host(ctl):
+    """ntm_mpc_step_ws (host buffers) == ntm_mpc_step_ws_device, workspace included."""
+    N, B = 20, 32
+    cfg, _ = cfgs(N, 2)
+    x0 = np.ascontiguousarray(O.scenario_x0(np.arange(B)).T)
+    rho, uo = ctl.initial_state(T(x0), cfg)
+    ws = ctl.new_active_ws(B, cfg)
+    rh, uh = H(rho).copy(), H(uo).copy()
+    wh = np.full((2 * (N + 1), B), -1, np.int32)
+    for _ in range(3):
+        dv = ctl.step(T(x0), rho, uo, cfg, active_ws=ws)
+        hs = ctl.step_host(x0, rh, uh, cfg, active_ws=wh)
+        np.testing.assert_array_equal(hs["U"], H(dv["U"]))
+        np.testing.assert_array_equal(wh, H(ws))
+        x0 = np.ascontiguousarray(hs["x_next"])
+    assert (wh[N] >= 0).all()                                          # slots hold active sets

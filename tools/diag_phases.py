@@ -12,11 +12,12 @@ lib = ntm_mpc.load()
 buf = (C.c_ulonglong * 16)()
 x = torch.tensor(ntm_mpc.scenarios_x0(0, B), device="cuda")
 rho, uo = ctl.initial_state(x, cfg)
-out = ctl.step(x, rho, uo, cfg); torch.cuda.synchronize()
+ws = ctl.new_active_ws(B, cfg)
+out = ctl.step(x, rho, uo, cfg, active_ws=ws); torch.cuda.synchronize()
 x = out["x_next"].clone()
 lib.ntm_debug_stamps(buf, 1)
 t = time.time()
-out = ctl.step(x, rho, uo, cfg); torch.cuda.synchronize()
+out = ctl.step(x, rho, uo, cfg, active_ws=ws); torch.cuda.synchronize()
 dt = time.time() - t
 assert lib.ntm_debug_stamps(buf, 1) == 0
 names = "lift cost scale cand regram gi polish roll gi_fact gi_check gi_dir gi_add gi_drop".split()
