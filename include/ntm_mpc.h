@@ -91,9 +91,9 @@ const char* ntm_last_error(const ntm_ctx* ctx);
  * 5 full Goldfarb-Idnani solves.  NULL disables. */
 #define NTM_STATS_ROWS 6
 int ntm_ctx_set_stats(ntm_ctx* ctx, int32_t* dev_stats);
-/* Diagnostic builds only: per-phase s_memtime cycle totals (16 counters);
+/* Diagnostic builds only: per-phase s_memtime cycle totals (32 counters);
  * NTM_E_UNSUPPORTED in production builds. */
-int ntm_debug_stamps(unsigned long long* out16, int reset);
+int ntm_debug_stamps(unsigned long long* out32, int reset);
 /* Launch shape the step/run kernels use for horizon N: lanes per scenario
  * (16/32/64) and the compile-time horizon of the specialisation (0 = generic). */
 int ntm_step_launch_info(int32_t N, int32_t* lanes, int32_t* horizon_template);

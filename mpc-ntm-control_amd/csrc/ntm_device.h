@@ -51,9 +51,10 @@ constexpr double kInf = __builtin_huge_val();
 // Diagnostic build only (-DNTM_STAMPS): per-phase s_memtime cycle totals,
 // summed over waves into ntm_stamps[] (read with ntm_debug_stamps).  The
 // production library compiles every stamp away.
+#define NTM_NSTAMPS 32
 #ifdef NTM_STAMPS
-extern __device__ unsigned long long ntm_stamps[16];
-__shared__ unsigned long long ntm_lds_stamps[16];   // per block (= per wave), flushed once
+extern __device__ unsigned long long ntm_stamps[NTM_NSTAMPS];
+__shared__ unsigned long long ntm_lds_stamps[NTM_NSTAMPS];   // per block (= per wave), flushed once
 #define NTM_T0(v) unsigned long long v = __builtin_amdgcn_s_memtime()
 #define NTM_ACC(i, v)                                                                   \
     do {                                                                                \
@@ -64,9 +65,9 @@ __shared__ unsigned long long ntm_lds_stamps[16];   // per block (= per wave), f
 #define NTM_CNT(i) \
     do { if ((threadIdx.x & 63) == 0) ntm_lds_stamps[i] += 1ull; } while (0)
 #define NTM_STAMPS_INIT() \
-    do { if (threadIdx.x < 16) ntm_lds_stamps[threadIdx.x] = 0; __syncthreads(); } while (0)
+    do { if (threadIdx.x < NTM_NSTAMPS) ntm_lds_stamps[threadIdx.x] = 0; __syncthreads(); } while (0)
 #define NTM_STAMPS_FLUSH() \
-    do { __syncthreads(); if (threadIdx.x < 16) atomicAdd(&ntm_stamps[threadIdx.x], ntm_lds_stamps[threadIdx.x]); } while (0)
+    do { __syncthreads(); if (threadIdx.x < NTM_NSTAMPS) atomicAdd(&ntm_stamps[threadIdx.x], ntm_lds_stamps[threadIdx.x]); } while (0)
 #else
 #define NTM_T0(v) (void)0
 #define NTM_ACC(i, v) (void)0
@@ -75,7 +76,8 @@ __shared__ unsigned long long ntm_lds_stamps[16];   // per block (= per wave), f
 #define NTM_STAMPS_FLUSH() (void)0
 #endif
 enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL, ST_GI_FACT, ST_GI_CHECK,
-       ST_GI_DIR, ST_GI_ADD, ST_GI_DROP, CN_CHECK, CN_CAND, CN_HIT };
+       ST_GI_DIR, ST_GI_ADD, ST_GI_DROP, CN_CHECK, CN_CAND, CN_HIT,
+       ST_P_CLASS, ST_P_GRAM, ST_P_CHOL, ST_P_SCHUR, ST_P_BWD, ST_P_KKT };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 
 #define NTM_WSYNC()                                              \
@@ -1275,6 +1277,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
     const int N = w.n(), LD = w.ldj(), LDJ = w.ldj();
     const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
     const double Vprev = (l < N) ? w.V()[l] : 0.0;
+    NTM_T0(tp);
     // --- classify active rows: single-entry rows fix a variable, the rest are general ---
     if (l < N) w.fx()[l] = 0;
     NTM_WSYNC();
@@ -1291,8 +1294,13 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
             nfix = -((lv * w.D()[j]) / w.D()[j]);
         } else {                                          // state row r = j: Lin = -+Gamma_r
             const double sg = (kind == 2) ? -1.0 : 1.0;
+            const int jm = j >> 1;
             int nnz = 0, jj = -1;
-            for (int c = 0; c <= (j >> 1); ++c) if (w.gt(j, c) != 0.0) { ++nnz; jj = c; }
+            // fixed trip count; gt(j, c) for c > j/2 still reads inside Gt (see check)
+            for (int c = 0; c < N; ++c) {
+                const double g = w.gt(j, c);
+                if (c <= jm && g != 0.0) { ++nnz; jj = c; }
+            }
             if (nnz == 1) {
                 double lv = sg * w.gt(j, jj);
                 fixj = jj;
@@ -1336,37 +1344,53 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
     const int nF = uni<P>((int)__popcll(bal));
     const int fpos = __popcll(bal & below);
     if (l < N && !fixed) w.fidx()[fpos] = l;
-    // --- z = Gamma U_B + e - r (scratch in w.xp(), rewritten by the rollout) ---
+    // --- y_B = Gamma U_B (fixed variables only; scratch in w.Phi(), dead until the
+    //     next lift) and z = y_B + e - r (scratch in w.xp(), rewritten by the rollout) ---
     for (int r = l; r < 2 * N; r += P) {
+        const int jm = r >> 1;
         double y = 0.0;
-        for (int j = 0; j <= (r >> 1); ++j)
-            if (w.fx()[j]) y += w.gt(r, j) * w.Uf()[j];
+        for (int j = 0; j < N; ++j) {
+            const double g = w.gt(r, j);
+            y += (j <= jm && w.fx()[j]) ? g * w.Uf()[j] : 0.0;
+        }
+        w.Phi()[r] = y;
         w.xp()[r] = y + w.e()[r] - pb.r[r & 1];
     }
     NTM_WSYNC();
-    // --- g_F (lane k = compact index) and the compact G~_FF (lower, col-major in R) ---
+    NTM_ACC(ST_P_CLASS, tp);
+    // --- g_F (lane a = compact index) ---
     double gl = 0.0;
     if (l < nF) {
         const int ja = w.fidx()[l];
-        const double* ca = w.Gt() + w.gidx(2 * ja, ja) - 2 * ja;
+        const double* ca = w.Gt() + w.gidx(2 * ja, ja) - 2 * ja;   // ca[r] = gt(r, ja), r >= 2 ja
         double g2 = 0.0;
-        for (int i = ja; i < N; ++i) {
-            double z0 = w.xp()[2 * i], z1 = w.xp()[2 * i + 1];
-            g2 += ca[2 * i] * (q00 * z0 + q01 * z1) + ca[2 * i + 1] * (q10 * z0 + q11 * z1);
+        for (int i = 0; i < N; ++i) {                               // terms i < ja masked
+            const double z0 = w.xp()[2 * i], z1 = w.xp()[2 * i + 1];
+            const double t = ca[2 * i] * (q00 * z0 + q01 * z1) + ca[2 * i + 1] * (q10 * z0 + q11 * z1);
+            g2 += (i >= ja) ? t : 0.0;
         }
         gl = w.D()[ja] * (2 * g2);
-        for (int c = 0; c <= l; ++c) {
-            const int jc = w.fidx()[c];
+    }
+    // --- compact G~_FF (lower, col-major in R): one (a, c) entry per lane ---
+    {
+        const int npair = nF * (nF + 1) / 2;
+        for (int idx = l; idx < npair; idx += P) {
+            int a = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
+            if ((a + 1) * (a + 2) / 2 <= idx) ++a;
+            if (a * (a + 1) / 2 > idx) --a;
+            const int c = idx - a * (a + 1) / 2;
+            const int ja = w.fidx()[a], jc = w.fidx()[c];            // ja >= jc
+            const double* ca = w.Gt() + w.gidx(2 * ja, ja) - 2 * ja;
             const double* cc = w.Gt() + w.gidx(2 * jc, jc) - 2 * jc;
             double sg = 0.0;
-            for (int i = ja; i < N; ++i) {
-                double g0 = cc[2 * i], g1 = cc[2 * i + 1];
-                double o0 = q00 * g0 + q01 * g1;
-                double o1 = q10 * g0 + q11 * g1;
-                sg += ca[2 * i] * o0;
-                sg += ca[2 * i + 1] * o1;
+            for (int i = 0; i < N; ++i) {                            // terms i < ja masked
+                const double g0 = cc[2 * i], g1 = cc[2 * i + 1];
+                const double o0 = q00 * g0 + q01 * g1;
+                const double o1 = q10 * g0 + q11 * g1;
+                const double t = ca[2 * i] * o0 + ca[2 * i + 1] * o1;
+                sg += (i >= ja) ? t : 0.0;
             }
-            w.R()[l + c * LD] = (2 * sg) * w.D()[ja] * w.D()[jc];
+            w.R()[a + c * LD] = (2 * sg) * w.D()[ja] * w.D()[jc];
         }
     }
     NTM_WSYNC();
@@ -1375,26 +1399,28 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
         const int r = w.srw()[s2];
         return (j <= (r >> 1)) ? -(((w.ssg()[s2] * w.gt(r, j)) * w.D()[j]) * w.irn()[r]) : 0.0;
     };
+    NTM_ACC(ST_P_GRAM, tp);
     bool ok = !collide && chol_inplace<P>(w.R(), nF, 1, LD, l, w.ldi());
     double vfin = 0.0;
     if (ok) {
         const double wl = fwd_lanes<P>(w.R(), w.ldi(), nF, 1, LD, gl, l);    // L^{-1} g_F
         double tl = -wl;
+        NTM_ACC(ST_P_CHOL, tp);
         if (nS > 0) {
-            // E' (compact rows) into Y = w.J() (row-major nF x nS) and h
-            if (l < nF) {
-                const int j = w.fidx()[l];
-                for (int s2 = 0; s2 < nS; ++s2) w.J()[l * LDJ + s2] = gen_n(s2, j);
-                w.d()[l] = wl;
+            // E' (compact rows) into Y = w.J() (row-major nF x nS), one entry per lane
+            for (int idx = l; idx < nF * nS; idx += P) {
+                const int a = idx / nS, s2 = idx - a * nS;
+                w.J()[a * LDJ + s2] = gen_n(s2, w.fidx()[a]);
             }
+            if (l < nF) w.d()[l] = wl;
+            // h_s = n_s' V = bc_s - n_s,B' V_B with n_s,B' V_B = -sg irn_r (Gamma_r U_B)
             double hs = 0.0;
             if (l < nS) {
                 const int r = w.srw()[l];
                 const int c = r & 1;
-                const double bval = (w.ssg()[l] > 0.0) ? (rows->xmax(c) - w.e()[r]) : (-rows->xmin(c) + w.e()[r]);
-                hs = -(bval * w.irn()[r]);
-                for (int j = 0; j <= (r >> 1); ++j)
-                    if (w.fx()[j]) hs -= gen_n(l, j) * w.Vb()[j];
+                const double sg = w.ssg()[l], ir = w.irn()[r];
+                const double bval = (sg > 0.0) ? (rows->xmax(c) - w.e()[r]) : (-rows->xmin(c) + w.e()[r]);
+                hs = -(bval * ir) + (sg * w.Phi()[r]) * ir;
             }
             NTM_WSYNC();
             if (l < nS) {                          // Y = L^{-1} E': lane s solves column s
@@ -1407,12 +1433,19 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
             NTM_WSYNC();
             double* K = w.R() + LD;                // K(a, c), a >= c, at R[c + (a+1) LD]
             double rhs = 0.0;
-            if (l < nS) {
-                for (int c = 0; c <= l; ++c) {
+            {
+                const int npair = nS * (nS + 1) / 2;
+                for (int idx = l; idx < npair; idx += P) {
+                    int a = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
+                    if ((a + 1) * (a + 2) / 2 <= idx) ++a;
+                    if (a * (a + 1) / 2 > idx) --a;
+                    const int c = idx - a * (a + 1) / 2;
                     double sK = 0.0;
-                    for (int i = 0; i < nF; ++i) sK += w.J()[i * LDJ + l] * w.J()[i * LDJ + c];
-                    K[l * LD + c] = sK;
+                    for (int i = 0; i < nF; ++i) sK += w.J()[i * LDJ + a] * w.J()[i * LDJ + c];
+                    K[a * LD + c] = sK;
                 }
+            }
+            if (l < nS) {
                 rhs = hs;
                 for (int i = 0; i < nF; ++i) rhs += w.J()[i * LDJ + l] * w.d()[i];
             }
@@ -1430,12 +1463,14 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
                 }
             }
         }
+        NTM_ACC(ST_P_SCHUR, tp);
         if (ok) {
             const double vF = bwd_lanes<P>(w.R(), w.ldi(), nF, 1, LD, tl, l);   // compact V_F
             const double vsc = __shfl(vF, (l < N && !fixed) ? fpos : 0, P);
             vfin = fixed ? vb : vsc;
         }
     }
+    NTM_ACC(ST_P_BWD, tp);
     if (ok) {
         // ---- KKT certificate ----
         if (l < N) { w.V()[l] = vfin; w.U()[l] = w.D()[l] * vfin; }
@@ -1445,8 +1480,12 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
         ok = vf.p == 0;
         // gradient G~V + F~ = D (2 Gamma' Om (Gamma D V) ) + F~ through Gamma
         for (int r = l; r < 2 * N; r += P) {
+            const int jm = r >> 1;
             double y = 0.0;
-            for (int j = 0; j <= (r >> 1); ++j) y += w.gt(r, j) * w.U()[j];
+            for (int j = 0; j < N; ++j) {
+                const double g = w.gt(r, j);
+                y += (j <= jm) ? g * w.U()[j] : 0.0;
+            }
             w.xp()[r] = y;
         }
         NTM_WSYNC();
@@ -1454,9 +1493,10 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
         if (l < N) {
             const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;
             double g2 = 0.0;
-            for (int i = l; i < N; ++i) {
-                double y0 = w.xp()[2 * i], y1 = w.xp()[2 * i + 1];
-                g2 += cl[2 * i] * (q00 * y0 + q01 * y1) + cl[2 * i + 1] * (q10 * y0 + q11 * y1);
+            for (int i = 0; i < N; ++i) {                            // terms i < l masked
+                const double y0 = w.xp()[2 * i], y1 = w.xp()[2 * i + 1];
+                const double t = cl[2 * i] * (q00 * y0 + q01 * y1) + cl[2 * i + 1] * (q10 * y0 + q11 * y1);
+                g2 += (i >= l) ? t : 0.0;
             }
             res = w.D()[l] * (2 * g2) + w.F()[l];
             for (int s2 = 0; s2 < nS; ++s2) res -= w.np()[s2] * gen_n(s2, l);
@@ -1474,6 +1514,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
         ok = ok && !(mmin < -1e-9 * fmax(1.0, mabs));
     }
     ok = gmaxi<P>(ok ? 0 : 1) == 0;
+    NTM_ACC(ST_P_KKT, tp);
     if (verify_only && !ok) {
         if (l < N) w.V()[l] = Vprev;
         NTM_WSYNC();

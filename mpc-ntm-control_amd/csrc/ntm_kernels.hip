@@ -23,7 +23,7 @@
 using namespace ntm;
 
 #ifdef NTM_STAMPS
-__device__ unsigned long long ntm::ntm_stamps[16];
+__device__ unsigned long long ntm::ntm_stamps[NTM_NSTAMPS];
 #endif
 
 namespace {
@@ -614,17 +614,17 @@ const char* ntm_last_error(const ntm_ctx* ctx) { return ctx ? ctx->err.c_str() :
 
 // Diagnostic builds (-DNTM_STAMPS) only: copy (and optionally reset) the
 // per-phase cycle totals; returns NTM_E_UNSUPPORTED in production builds.
-int ntm_debug_stamps(unsigned long long* out16, int reset) {
+int ntm_debug_stamps(unsigned long long* out32, int reset) {
 #ifdef NTM_STAMPS
-    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(ntm::ntm_stamps), 16 * sizeof(unsigned long long)) != hipSuccess)
+    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(ntm::ntm_stamps), NTM_NSTAMPS * sizeof(unsigned long long)) != hipSuccess)
         return NTM_E_DEVICE;
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[NTM_NSTAMPS] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(ntm::ntm_stamps), z, sizeof z) != hipSuccess) return NTM_E_DEVICE;
     }
     return NTM_OK;
 #else
-    (void)out16;
+    (void)out32;
     (void)reset;
     return NTM_E_UNSUPPORTED;
 #endif

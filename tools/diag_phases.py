@@ -9,7 +9,7 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 cfg = Config(N=20, mode=2)
 ctl = NtmMpc(config=cfg)
 lib = ntm_mpc.load()
-buf = (C.c_ulonglong * 16)()
+buf = (C.c_ulonglong * 32)()
 x = torch.tensor(ntm_mpc.scenarios_x0(0, B), device="cuda")
 rho, uo = ctl.initial_state(x, cfg)
 ws = ctl.new_active_ws(B, cfg)
@@ -26,3 +26,7 @@ print(f"B={B} step {dt*1e3:.1f} ms; cycles per wave-step by phase (s_memtime):")
 for i, n in enumerate(names):
     print(f"  {n:9s} {buf[i]/B:12.0f}  {100*buf[i]/tot:5.1f}%")
 print(f"per wave-step: check calls {buf[13]/B:.1f}, candidate tries {buf[14]/B:.2f}, hits {buf[15]/B:.2f}")
+sub = "p_class p_gram p_chol p_schur p_bwd p_kkt".split()
+print("certified re-solve (cand + polish) sub-phases, cycles per wave-step:")
+for i, n in enumerate(sub):
+    print(f"  {n:9s} {buf[16 + i]/B:12.0f}")
