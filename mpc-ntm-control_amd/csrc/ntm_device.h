@@ -77,8 +77,9 @@ __shared__ unsigned long long ntm_lds_stamps[NTM_NSTAMPS];   // per block (= per
 #endif
 enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL, ST_GI_FACT, ST_GI_CHECK,
        ST_GI_DIR, ST_GI_ADD, ST_GI_DROP, CN_CHECK, CN_CAND, CN_HIT,
-       ST_P_CLASS, ST_P_GRAM, ST_P_CHOL, ST_P_SCHUR, ST_P_BWD, ST_P_KKT };
+       ST_P_CLASS, ST_P_GRAM, ST_P_CHOL, ST_P_SCHUR, ST_P_BWD, ST_P_KKT, CN_REPAIR, CN_GIRUN };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
+constexpr int kRepairs = 8;        // single-row repairs of a failed warm-start candidate
 
 #define NTM_WSYNC()                                              \
     do {                                                         \
@@ -1273,7 +1274,8 @@ __device__ bool polish_phase(const Prob& pb, const W& w, const Rows* rows, int q
 // ---------------------------------------------------------------------------
 template <int P, class W>
 __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* rows, int q, int l, bool verify_only,
-                               int* ns_out) {
+                               int* ns_out, int* fail_kind = nullptr, int* fail_pos = nullptr,
+                               double* v_out = nullptr) {
     const int N = w.n(), LD = w.ldj(), LDJ = w.ldj();
     const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
     const double Vprev = (l < N) ? w.V()[l] : 0.0;
@@ -1322,7 +1324,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
     if (l < q) {
         if (isgen) {
             const int k = __popcll(bal & below);
-            w.sidx()[k] = id;
+            w.sidx()[k] = l;                              // its position in the active list
             w.srw()[k] = srow;
             w.ssg()[k] = ssign;
         } else {
@@ -1401,6 +1403,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
     };
     NTM_ACC(ST_P_GRAM, tp);
     bool ok = !collide && chol_inplace<P>(w.R(), nF, 1, LD, l, w.ldi());
+    int fk = ok ? 0 : 3, fpos_out = 0;
     double vfin = 0.0;
     if (ok) {
         const double wl = fwd_lanes<P>(w.R(), w.ldi(), nF, 1, LD, gl, l);    // L^{-1} g_F
@@ -1451,6 +1454,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
             }
             NTM_WSYNC();
             ok = chol_inplace<P>(K, nS, LD, 1, l, w.kdi());
+            if (!ok) fk = 3;
             if (ok) {
                 double t1 = fwd_lanes<P>(K, w.kdi(), nS, LD, 1, rhs, l);
                 double mu = bwd_lanes<P>(K, w.kdi(), nS, LD, 1, t1, l);
@@ -1501,20 +1505,30 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
             res = w.D()[l] * (2 * g2) + w.F()[l];
             for (int s2 = 0; s2 < nS; ++s2) res -= w.np()[s2] * gen_n(s2, l);
         }
+        // multipliers: general row s on lane s, fixed variable j on lane j; each
+        // lane keeps its most negative one and that row's active-list position
         double mval = 0.0;
+        int mpos = 0x7fffffff;
         bool has = false;
-        if (l < nS) { mval = w.np()[l]; has = true; }
+        if (l < nS) { mval = w.np()[l]; mpos = w.sidx()[l]; has = true; }
         if (fixed) {
             double lam = res / w.hv()[l];
-            mval = has ? fmin(mval, lam) : lam;
+            if (!has || lam < mval) { mval = lam; mpos = w.fx()[l] - 1; }
             has = true;
         }
         double mabs = gmax<P>(has ? fabs(mval) : 0.0);
-        double mmin = -gmax<P>(has ? -mval : -kInf);
-        ok = ok && !(mmin < -1e-9 * fmax(1.0, mabs));
+        double mkey = has ? mval : kInf;
+        gargmin<P>(mkey, mpos);
+        const bool dual_ok = !(mkey < -1e-9 * fmax(1.0, mabs));
+        fk = !ok ? 2 : (!dual_ok ? 1 : 0);
+        fpos_out = mpos;
+        ok = ok && dual_ok;
     }
     ok = gmaxi<P>(ok ? 0 : 1) == 0;
     NTM_ACC(ST_P_KKT, tp);
+    if (fail_kind) *fail_kind = uni<P>(fk);
+    if (fail_pos) *fail_pos = uni<P>(fpos_out);
+    if (v_out) *v_out = vfin;
     if (verify_only && !ok) {
         if (l < N) w.V()[l] = Vprev;
         NTM_WSYNC();
@@ -1613,19 +1627,56 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
             // so the active set of iteration it-2 is tried first; it is taken
             // only if the exact active-set solve passes the KKT certificate
             // (the optimum of this strictly convex QP is unique).
-            const int cq = uni<P>(cand[N]);
-            if (cq >= 0) {
+            const int cq0 = uni<P>(cand[N]);
+            if (cq0 >= 0) {
                 NTM_CNT(CN_CAND);
-                if (n_try) ++*n_try;
+                int cq = cq0;
                 if (l < cq) w.act()[l] = cand[l];
                 NTM_WSYNC();
-                if (polish_compact<P>(pb, w, &rows, cq, l, true, &ns)) {
-                    flag = NTM_EXIT_OPTIMAL;
-                    q = cq;
-                    done = true;
-                    NTM_CNT(CN_HIT);
-                } else {
-                    if (l < cq) w.aflag()[cand[l]] = kCandRow;
+                // certified re-solve of the candidate; on failure, up to kRepairs
+                // single-row repairs (add the most violated row, or drop the row
+                // with the most negative multiplier) before falling back to GI.
+                // Only a set that passes the KKT certificate is ever accepted.
+                for (int rep = 0;; ++rep) {
+                    if (n_try) ++*n_try;
+                    int fk = 0, fp = 0;
+                    double vf = 0.0;
+                    if (polish_compact<P>(pb, w, &rows, cq, l, true, &ns, &fk, &fp, &vf)) {
+                        flag = NTM_EXIT_OPTIMAL;
+                        q = cq;
+                        done = true;
+                        NTM_CNT(CN_HIT);
+                        if (rep > 0) NTM_CNT(CN_REPAIR);
+                        break;
+                    }
+                    if (rep == kRepairs || fk == 3) break;
+                    if (fk == 2) {                         // primal: add the most violated row
+                        if (l < cq) w.aflag()[w.act()[l]] = kActiveRow;
+                        NTM_WSYNC();
+                        const double vmx = gmax<P>(l < N ? fabs(vf) : 0.0);
+                        const Pick pk = rows.template check<P>(w, vf, l, false, fmax(1.0, vmx));
+                        NTM_WSYNC();
+                        if (l < cq) w.aflag()[w.act()[l]] = 0;
+                        NTM_WSYNC();
+                        if (pk.p < 0) break;
+                        if (cq < N) {
+                            if (l == 0) w.act()[cq] = pk.p;
+                            ++cq;
+                        } else if (l == 0) {               // full set: swap out the smallest multiplier
+                            w.act()[fp] = pk.p;
+                        }
+                    } else {                               // dual: drop position fp
+                        int an = 0;
+                        if (l >= fp && l + 1 < cq) an = w.act()[l + 1];
+                        NTM_WSYNC();
+                        if (l >= fp && l + 1 < cq) w.act()[l] = an;
+                        --cq;
+                    }
+                    NTM_WSYNC();
+                }
+                if (!done) {
+                    // the repaired set steers GI's add order (StructRows::check)
+                    if (l < cq) w.aflag()[w.act()[l]] = kCandRow;
                     NTM_WSYNC();
                 }
                 NTM_ACC(ST_CAND, tq);
@@ -1636,6 +1687,7 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                 } else {
                     NTM_ACC(ST_REGRAM, tq);
                     if (n_girun) ++*n_girun;
+                    NTM_CNT(CN_GIRUN);
                     flag = gi_solve<P, StructRows, W>(w, pb.mode == NTM_MODE_NONE ? nullptr : &rows, nrows, l,
                                                       qp_iters, &q);
                     NTM_ACC(ST_GI, tq);

@@ -25,7 +25,7 @@ tot = sum(buf[i] for i in range(8))
 print(f"B={B} step {dt*1e3:.1f} ms; cycles per wave-step by phase (s_memtime):")
 for i, n in enumerate(names):
     print(f"  {n:9s} {buf[i]/B:12.0f}  {100*buf[i]/tot:5.1f}%")
-print(f"per wave-step: check calls {buf[13]/B:.1f}, candidate tries {buf[14]/B:.2f}, hits {buf[15]/B:.2f}")
+print(f"per wave-step: check calls {buf[13]/B:.1f}, candidate sets {buf[14]/B:.2f}, hits {buf[15]/B:.2f} (after repair {buf[22]/B:.2f}), GI solves {buf[23]/B:.2f}")
 sub = "p_class p_gram p_chol p_schur p_bwd p_kkt".split()
 print("certified re-solve (cand + polish) sub-phases, cycles per wave-step:")
 for i, n in enumerate(sub):
