@@ -583,17 +583,17 @@ struct StructRows {
     int N, mode;  // mode: NTM_MODE_BOX or NTM_MODE_FULL (NONE: no rows)
     double umin, umax, xmin0, xmin1, xmax0, xmax1;
 
-    __device__ StructRows(const Prob& p)
+    __device__ __forceinline__ StructRows(const Prob& p)
         : N(p.N), mode(p.mode), umin(p.umin), umax(p.umax), xmin0(p.xmin[0]), xmin1(p.xmin[1]),
           xmax0(p.xmax[0]), xmax1(p.xmax[1]) {}
     __device__ __forceinline__ double xmin(int c) const { return c ? xmin1 : xmin0; }
     __device__ __forceinline__ double xmax(int c) const { return c ? xmax1 : xmax0; }
 
-    __device__ int rows() const { return mode == NTM_MODE_BOX ? 2 * N : 6 * N + 4; }
+    __device__ __forceinline__ int rows() const { return mode == NTM_MODE_BOX ? 2 * N : 6 * N + 4; }
 
     // decode a row id: kind 0 = u lower, 1 = u upper, 2 = state min, 3 = state max;
     // j = variable (u rows) or state row r (state rows); -1 for x_0 rows
-    __device__ void decode(int id, int N, int& kind, int& j) const {
+    __device__ __forceinline__ void decode(int id, int N, int& kind, int& j) const {
         if (mode == NTM_MODE_BOX) {
             kind = id < N ? 0 : 1;
             j = id < N ? id : id - N;
@@ -609,14 +609,14 @@ struct StructRows {
         j = (i == 0) ? -1 : 2 * (i - 1) + c;
     }
     // u-bound row: its variable j and the sign of its GI normal (+1 lower, -1 upper); -1 otherwise
-    __device__ int unit_row(int id, int Nn, double& sg) const {
+    __device__ __forceinline__ int unit_row(int id, int Nn, double& sg) const {
         int kind, j;
         decode(id, Nn, kind, j);
         sg = (kind == 0) ? 1.0 : -1.0;
         return kind < 2 ? j : -1;
     }
     template <class W>
-    __device__ double lin(const W& w, int id, int col) const {          // Lin[id][col]
+    __device__ __forceinline__ double lin(const W& w, int id, int col) const {          // Lin[id][col]
         int kind, j;
         decode(id, w.n(), kind, j);
         if (kind < 2) return (col == j) ? (kind == 0 ? -1.0 : 1.0) : 0.0;
@@ -625,7 +625,7 @@ struct StructRows {
         return kind == 2 ? -g : g;
     }
     template <class W>
-    __device__ double bval(const W& w, int id) const {                  // b[id]
+    __device__ __forceinline__ double bval(const W& w, int id) const {                  // b[id]
         int kind, j;
         decode(id, w.n(), kind, j);
         if (kind == 0) return -umin;
@@ -634,7 +634,7 @@ struct StructRows {
         return kind == 2 ? (-xmin(c) + w.e()[j]) : (xmax(c) - w.e()[j]);
     }
     template <class W>
-    __device__ double rnorm(const W& w, int id) const {
+    __device__ __forceinline__ double rnorm(const W& w, int id) const {
         int kind, j;
         decode(id, w.n(), kind, j);
         return kind < 2 ? w.D()[j] : w.rn()[j];
@@ -642,7 +642,7 @@ struct StructRows {
 
     // constant rows (x_0 rows; state rows with Gamma_r == 0): 0 <= b or infeasible (D15)
     template <int P, class W>
-    __device__ bool feasible_const(const W& w, double x0, double x1, int l) const {
+    __device__ __forceinline__ bool feasible_const(const W& w, double x0, double x1, int l) const {
         int bad = 0;
         if (mode == NTM_MODE_FULL) {
             if (l == 0) {
@@ -669,7 +669,7 @@ struct StructRows {
     // GI's stopping tolerance: GI may add any violated row, so this only
     // steers it towards the nearby active set.
     template <int P, class W>
-    __device__ Pick check(const W& w, double Vl, int l, bool verify = false, double vmax = 1.0) const {
+    __device__ __forceinline__ Pick check(const W& w, double Vl, int l, bool verify = false, double vmax = 1.0) const {
         const int N = w.n();
         if (mode == NTM_MODE_NONE) { Pick none; none.p = verify ? 0 : -1; none.s = 0.0; none.bc = 0.0; return none; }
         double bv = kInf, bs = 0.0, bbc = 0.0;
@@ -727,7 +727,7 @@ struct StructRows {
 
     // GI normal n_p into w.np(); returns bc_p
     template <int P, class W>
-    __device__ double load_np(const W& w, int p, int l) const {
+    __device__ __forceinline__ double load_np(const W& w, int p, int l) const {
         double rn = rnorm(w, p);
         if (l < w.n()) w.np()[l] = -((lin(w, p, l) * w.D()[l]) / rn);
         NTM_WSYNC();
@@ -864,7 +864,7 @@ __device__ double bwd_lanes(const double* L, const double* rdiag, int n, int RS,
 // (Goldfarb & Idnani 1983, section 3).
 // ---------------------------------------------------------------------------
 template <int P, class Rows, class W>
-__device__ int gi_solve(const W& w, const Rows* rows, int nrows, int l, int* iters_out, int* q_out) {
+__device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, int l, int* iters_out, int* q_out) {
     const int N = w.n(), LD = w.ldj(), LDJ = w.ldj();
     *iters_out = 0;
     *q_out = 0;
@@ -901,13 +901,13 @@ __device__ int gi_solve(const W& w, const Rows* rows, int nrows, int l, int* ite
         NTM_WSYNC();
     }
     NTM_ACC(ST_GI_FACT, tg);
-    if (!rows) return NTM_EXIT_OPTIMAL;
+    if (!has_rows) return NTM_EXIT_OPTIMAL;
     if (l < N) for (int b = 0; b < N; ++b) w.T()[l * LDJ + b] = 0.0;
     const int max_iter = 10 * (N + nrows) + 50;
     int q = 0, it = 0;
     for (;;) {
         const double vmax = gmax<P>(l < N ? fabs(Vl) : 0.0);
-        Pick pk = rows->template check<P>(w, Vl, l, false, fmax(1.0, vmax));
+        Pick pk = rows.template check<P>(w, Vl, l, false, fmax(1.0, vmax));
         NTM_ACC(ST_GI_CHECK, tg);
         NTM_CNT(CN_CHECK);
         if (pk.p < 0 || pk.s >= -1e-12 * fmax(fmax(1.0, vmax), fabs(pk.bc))) {
@@ -916,12 +916,12 @@ __device__ int gi_solve(const W& w, const Rows* rows, int nrows, int l, int* ite
             return NTM_EXIT_OPTIMAL;
         }
         const int p = pk.p;
-        const double bcp = uni<P>(rows->template load_np<P>(w, p, l));
+        const double bcp = uni<P>(rows.template load_np<P>(w, p, l));
         // u-bound rows have n_p = -+e_j: d = J' n_p is then a signed row of J
         int ej = -1;
         double esg = 0.0;
         if constexpr (Rows::kHasUnitRows) {
-            ej = uni<P>(rows->unit_row(p, N, esg));
+            ej = uni<P>(rows.unit_row(p, N, esg));
             esg = uni<P>(esg);
         }
         double upq = 0.0;   // multiplier of the constraint being added
@@ -1273,7 +1273,7 @@ __device__ bool polish_phase(const Prob& pb, const W& w, const Rows* rows, int q
 // when !verify_only (then GI's V is kept); returns success.
 // ---------------------------------------------------------------------------
 template <int P, class W>
-__device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* rows, int q, int l, bool verify_only,
+__device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows, int q, int l, bool verify_only,
                                int* ns_out, int* fail_kind = nullptr, int* fail_pos = nullptr,
                                double* v_out = nullptr) {
     const int N = w.n(), LD = w.ldj(), LDJ = w.ldj();
@@ -1288,11 +1288,11 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
     if (l < q) {
         id = w.act()[l];
         int kind, j;
-        rows->decode(id, N, kind, j);
+        rows.decode(id, N, kind, j);
         if (kind < 2) {                                   // u bound: Lin = -+e_j, b = -umin / umax
             fixj = j;
             double lv = kind == 0 ? -1.0 : 1.0;
-            ufix = rows->bval(w, id) / lv;
+            ufix = rows.bval(w, id) / lv;
             nfix = -((lv * w.D()[j]) / w.D()[j]);
         } else {                                          // state row r = j: Lin = -+Gamma_r
             const double sg = (kind == 2) ? -1.0 : 1.0;
@@ -1306,7 +1306,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
             if (nnz == 1) {
                 double lv = sg * w.gt(j, jj);
                 fixj = jj;
-                ufix = rows->bval(w, id) / lv;
+                ufix = rows.bval(w, id) / lv;
                 nfix = -((lv * w.D()[jj]) / w.rn()[j]);
             } else {
                 isgen = 1;
@@ -1356,7 +1356,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
             y += (j <= jm && w.fx()[j]) ? g * w.Uf()[j] : 0.0;
         }
         w.Phi()[r] = y;
-        w.xp()[r] = y + w.e()[r] - pb.r[r & 1];
+        w.xp()[r] = y + w.e()[r] - ((r & 1) ? pb.r[1] : pb.r[0]);
     }
     NTM_WSYNC();
     NTM_ACC(ST_P_CLASS, tp);
@@ -1422,7 +1422,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
                 const int r = w.srw()[l];
                 const int c = r & 1;
                 const double sg = w.ssg()[l], ir = w.irn()[r];
-                const double bval = (sg > 0.0) ? (rows->xmax(c) - w.e()[r]) : (-rows->xmin(c) + w.e()[r]);
+                const double bval = (sg > 0.0) ? (rows.xmax(c) - w.e()[r]) : (-rows.xmin(c) + w.e()[r]);
                 hs = -(bval * ir) + (sg * w.Phi()[r]) * ir;
             }
             NTM_WSYNC();
@@ -1480,7 +1480,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows* row
         if (l < N) { w.V()[l] = vfin; w.U()[l] = w.D()[l] * vfin; }
         NTM_WSYNC();
         double vmax = gmax<P>(l < N ? fabs(vfin) : 0.0);
-        Pick vf = rows->template check<P>(w, vfin, l, true, fmax(1.0, vmax));
+        Pick vf = rows.template check<P>(w, vfin, l, true, fmax(1.0, vmax));
         ok = vf.p == 0;
         // gradient G~V + F~ = D (2 Gamma' Om (Gamma D V) ) + F~ through Gamma
         for (int r = l; r < 2 * N; r += P) {
@@ -1641,7 +1641,7 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                     if (n_try) ++*n_try;
                     int fk = 0, fp = 0;
                     double vf = 0.0;
-                    if (polish_compact<P>(pb, w, &rows, cq, l, true, &ns, &fk, &fp, &vf)) {
+                    if (polish_compact<P>(pb, w, rows, cq, l, true, &ns, &fk, &fp, &vf)) {
                         flag = NTM_EXIT_OPTIMAL;
                         q = cq;
                         done = true;
@@ -1688,10 +1688,10 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                     NTM_ACC(ST_REGRAM, tq);
                     if (n_girun) ++*n_girun;
                     NTM_CNT(CN_GIRUN);
-                    flag = gi_solve<P, StructRows, W>(w, pb.mode == NTM_MODE_NONE ? nullptr : &rows, nrows, l,
+                    flag = gi_solve<P, StructRows, W>(w, rows, pb.mode != NTM_MODE_NONE, nrows, l,
                                                       qp_iters, &q);
                     NTM_ACC(ST_GI, tq);
-                    if (flag == NTM_EXIT_OPTIMAL) (void)polish_compact<P>(pb, w, &rows, q, l, false, &ns);
+                    if (flag == NTM_EXIT_OPTIMAL) (void)polish_compact<P>(pb, w, rows, q, l, false, &ns);
                     NTM_ACC(ST_POLISH, tq);
                 }
             }

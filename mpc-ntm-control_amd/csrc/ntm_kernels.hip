@@ -365,7 +365,7 @@ __global__ __launch_bounds__(64) void k_qp(int64_t B, int N, int m, const double
             // keep G~ for the polish (w.Gt() is unused without a lifted model)
             if (l < N) for (int j = 0; j <= l; ++j) gsave[l + j * w.ldj()] = w.R()[l + j * w.ldj()];
             NTM_WSYNC();
-            flag = gi_solve<P, DenseRows, decltype(w)>(w, m > 0 ? &rows : nullptr, m, l, &its, &q);
+            flag = gi_solve<P, DenseRows, decltype(w)>(w, rows, m > 0, m, l, &its, &q);
         }
     }
     if (flag == NTM_EXIT_OPTIMAL) {
