@@ -358,13 +358,15 @@ __device__ void lift_phase(const Prob& pb, const W& w, int l) {
         double g0 = w.bb()[l], g1 = 0.0;
         col[2 * l] = g0;
         col[2 * l + 1] = g1;
-        for (int i = l + 1; i < N; ++i) {
-            double n0 = w.a11()[i] * g0;
-            double n1 = w.a21()[i] * g0 + k.a22 * g1;
-            g0 = n0;
-            g1 = n1;
-            col[2 * i] = g0;
-            col[2 * i + 1] = g1;
+        for (int i = 1; i < N; ++i) {        // fixed trip count (unrolls), branch-free:
+            const double n0 = w.a11()[i] * g0;   // rows i <= l keep (B_l, 0) and rewrite
+            const double n1 = w.a21()[i] * g0 + k.a22 * g1;   // the column's own diagonal
+            const bool live = i > l;
+            g0 = live ? n0 : g0;
+            g1 = live ? n1 : g1;
+            const int ii = live ? i : l;
+            col[2 * ii] = g0;
+            col[2 * ii + 1] = g1;
         }
     }
     // Phi (left-multiplied, D4) and Lambda: short sequential chains on lane 0
@@ -408,20 +410,25 @@ template <int P, class W>
 __device__ void gram_rows(const Prob& pb, const W& w, double* dst, int l) {
     const int N = w.n(), LD = w.ldj();
     const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
-    if (l < N) {
-        const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
-        for (int kk = 0; kk <= l; ++kk) {
-            const double* ck = w.Gt() + w.gidx(2 * kk, kk) - 2 * kk;
-            double s = 0.0;
-            for (int i = l; i < N; ++i) {
-                double g0 = ck[2 * i], g1 = ck[2 * i + 1];
-                double o0 = q00 * g0 + q01 * g1;
-                double o1 = q10 * g0 + q11 * g1;
-                s += cj[2 * i] * o0;
-                s += cj[2 * i + 1] * o1;
-            }
-            dst[l + kk * LD] = 2 * s;   // G(l, kk), l >= kk
+    // one (j, kk) entry per lane; fixed-trip masked dot (column reads below the
+    // packed column start stay inside Gt, see StructRows::check)
+    const int npair = N * (N + 1) / 2;
+    for (int idx = l; idx < npair; idx += P) {
+        int j = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
+        if ((j + 1) * (j + 2) / 2 <= idx) ++j;
+        if (j * (j + 1) / 2 > idx) --j;
+        const int kk = idx - j * (j + 1) / 2;
+        const double* cj = w.Gt() + w.gidx(2 * j, j) - 2 * j;
+        const double* ck = w.Gt() + w.gidx(2 * kk, kk) - 2 * kk;
+        double s = 0.0;
+        for (int i = 0; i < N; ++i) {
+            const double g0 = ck[2 * i], g1 = ck[2 * i + 1];
+            const double o0 = q00 * g0 + q01 * g1;
+            const double o1 = q10 * g0 + q11 * g1;
+            const double t = cj[2 * i] * o0 + cj[2 * i + 1] * o1;
+            s += (i >= j) ? t : 0.0;
         }
+        dst[j + kk * LD] = 2 * s;   // G(j, kk), j >= kk
     }
 }
 
@@ -476,13 +483,13 @@ __device__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_st
     if (l < N) {
         const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
         double s = 0.0;
-        for (int i = l; i < N; ++i) {
-            double g0 = cj[2 * i], g1 = cj[2 * i + 1];
-            bad |= !isfinite(g0) || !isfinite(g1);
-            double o0 = q00 * g0 + q01 * g1;
-            double o1 = q10 * g0 + q11 * g1;
-            s += g0 * o0;
-            s += g1 * o1;
+        for (int i = 0; i < N; ++i) {            // fixed trip count, terms i < l masked
+            const double g0 = cj[2 * i], g1 = cj[2 * i + 1];
+            const double o0 = q00 * g0 + q01 * g1;
+            const double o1 = q10 * g0 + q11 * g1;
+            const double t = g0 * o0 + g1 * o1;
+            if (i >= l) bad |= !isfinite(g0) || !isfinite(g1);
+            s += (i >= l) ? t : 0.0;
         }
         double g = 2 * s;
         double Dl = (g > 0.0) ? 1.0 / sqrt(g) : 1.0;
@@ -498,8 +505,11 @@ __device__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_st
     if (with_state_rows) {
         for (int r = l; r < 2 * N; r += P) {
             double s = 0.0;
-            int jmax = r >> 1;
-            for (int j = 0; j <= jmax; ++j) { double v = w.gt(r, j) * w.D()[j]; s += v * v; }
+            const int jmax = r >> 1;
+            for (int j = 0; j < N; ++j) {        // fixed trip count, j > jmax masked
+                const double v = w.gt(r, j) * w.D()[j];
+                s += (j <= jmax) ? v * v : 0.0;
+            }
             bad |= !isfinite(s) || !isfinite(w.e()[r]);
             double rn = s > 0.0 ? sqrt(s) : 0.0;
             w.rn()[r] = rn;
@@ -548,11 +558,12 @@ __device__ void f_phase(const Prob& pb, const W& w, int l) {
     if (l < N) {
         const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
         double f = 0.0;
-        for (int i = l; i < N; ++i) {
-            double e0 = w.e()[2 * i] - pb.r[0], e1 = w.e()[2 * i + 1] - pb.r[1];
-            double o0 = q00 * e0 + q01 * e1;
-            double o1 = q10 * e0 + q11 * e1;
-            f += cj[2 * i] * o0 + cj[2 * i + 1] * o1;
+        for (int i = 0; i < N; ++i) {            // fixed trip count, terms i < l masked
+            const double e0 = w.e()[2 * i] - pb.r[0], e1 = w.e()[2 * i + 1] - pb.r[1];
+            const double o0 = q00 * e0 + q01 * e1;
+            const double o1 = q10 * e0 + q11 * e1;
+            const double t = cj[2 * i] * o0 + cj[2 * i + 1] * o1;
+            f += (i >= l) ? t : 0.0;
         }
         w.F()[l] = 2 * f;
     }
