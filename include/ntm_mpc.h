@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define NTM_MPC_ABI_VERSION 1
+#define NTM_MPC_ABI_VERSION 2
 #define NTM_MAX_N 64
 
 /* Physics constants, NTM_MPC_Sim.m:5-22 (same names and units). */
@@ -44,7 +44,12 @@ typedef struct {
 /* Constraint modes. */
 enum { NTM_MODE_NONE = 0,   /* unconstrained LQ (BASELINE config 1)       */
        NTM_MODE_BOX = 1,    /* u in [umin, umax] only (config 2)          */
-       NTM_MODE_FULL = 2 }; /* full getWLc.m polyhedron, m = 6N+4 (cfg 3) */
+       NTM_MODE_FULL = 2,   /* full getWLc.m polyhedron, m = 6N+4 (cfg 3) */
+       NTM_MODE_FULL_DU = 3 }; /* getWLc rows + input-rate rows
+                                *   |U_i - U_{i-1}| <= du_max, i = 1..N-1,
+                                * m = 8N+2 (BASELINE config 5; an extension
+                                * of getWLc.m's row structure, not in the
+                                * reference) */
 
 /* Literal-reference switches; 0 = canonical semantics. */
 enum { NTM_LITERAL_PHI_RIGHTMUL = 1 << 0,  /* D4  Rho_to_PhiGammaLambda.m:21 */
@@ -65,6 +70,7 @@ typedef struct {
     double Q[4];        /* :59 state weight, row-major 2x2, symmetric PSD  */
     double r[2];        /* :60 reference state                             */
     double epsilon;     /* :87 convergence threshold on sum|U - Uold|      */
+    double du_max;      /* NTM_MODE_FULL_DU only: input-rate bound (W/step) */
 } ntm_config;
 
 /* Return codes. */

@@ -42,11 +42,32 @@ struct Prob {
     Coef k;
     int N, i_sim, mode, flags;
     double xmin[2], xmax[2], umin, umax, Q[4], r[2], eps;
+    double du;        // input-rate bound (NTM_MODE_FULL_DU)
     int32_t* stats;   // optional per-scenario counters (4 x B, SoA): QP solves,
                       // GI iterations, final active rows, general (state) active rows
 };
 
 constexpr double kInf = __builtin_huge_val();
+
+// Trace build only (make trace NTM_DEBUG_SCEN=s): printf GI's iterations for
+// one scenario.  The production library compiles every trace away.
+#ifdef NTM_DEBUG_SCEN
+__shared__ int ntm_trace_grp;   // group (of this one-wave block) that owns the traced scenario
+#define NTM_TRACE_SET(s, g, l)                                                  \
+    do {                                                                        \
+        if (threadIdx.x == 0) ntm_trace_grp = -1;                               \
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");                 \
+        __builtin_amdgcn_wave_barrier();                                        \
+        if ((l) == 0 && (s) == NTM_DEBUG_SCEN) ntm_trace_grp = (g);             \
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");                 \
+        __builtin_amdgcn_wave_barrier();                                        \
+    } while (0)
+#define NTM_TRACE(...) \
+    do { if (ntm_trace_grp == (int)((threadIdx.x & 63) / P) && l == 0) printf(__VA_ARGS__); } while (0)
+#else
+#define NTM_TRACE_SET(s, g, l) (void)0
+#define NTM_TRACE(...) (void)0
+#endif
 
 // Diagnostic build only (-DNTM_STAMPS): per-phase s_memtime cycle totals,
 // summed over waves into ntm_stamps[] (read with ntm_debug_stamps).  The
@@ -311,7 +332,8 @@ struct WS {
     __device__ __forceinline__ double* ldi() const { return base + oV() + 20 * n() + 3; }   // N: 1/L(k,k) (Cholesky)
     __device__ __forceinline__ double* kdi() const { return base + oV() + 21 * n() + 3; }   // N: 1/K(k,k) (Schur)
     __device__ __forceinline__ double* ssg() const { return base + oV() + 22 * n() + 3; }   // N: sign of general row s
-    __device__ __forceinline__ int* act() const { return reinterpret_cast<int*>(base + oV() + 23 * n() + 3); }
+    __device__ __forceinline__ double* idun() const { return base + oV() + 23 * n() + 3; }  // N: 1/|D (e_i - e_{i-1})|
+    __device__ __forceinline__ int* act() const { return reinterpret_cast<int*>(base + oV() + 24 * n() + 3); }
     __device__ __forceinline__ int* sidx() const { return act() + n() + 1; }
     __device__ __forceinline__ int* cand() const { return act() + 2 * (n() + 1); }   // 2(n()+1): last two active sets
     __device__ __forceinline__ int* fidx() const { return act() + 4 * (n() + 1); }   // n()+1: free variables (polish)
@@ -324,10 +346,10 @@ struct WS {
 
 __host__ __device__ inline int ldj_of(int N) { return N | 1; }
 __host__ __device__ inline int ws_doubles(int N) {
-    return 14 * N + N * (N + 1) + 2 * N * ldj_of(N) + (N + 1) * ldj_of(N) + 23 * N + 3;
+    return 14 * N + N * (N + 1) + 2 * N * ldj_of(N) + (N + 1) * ldj_of(N) + 24 * N + 3;
 }
 __host__ __device__ inline int ws_bytes(int N) {
-    int b = ws_doubles(N) * 8 + 6 * (N + 1) * 4 + N + (6 * NTM_MAX_N + 4);
+    int b = ws_doubles(N) * 8 + 6 * (N + 1) * 4 + N + (8 * N + 4);   // ..., fx (N), aflag (rows <= 8N+2)
     return (b + 15) & ~15;
 }
 
@@ -502,6 +524,10 @@ __device__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_st
         w.vhi()[l] = pb.umax / Dl;
     }
     NTM_WSYNC();
+    if (pb.mode == NTM_MODE_FULL_DU && l >= 1 && l < N) {      // rate-row norms |D (e_l - e_{l-1})|
+        const double a = w.D()[l], b = w.D()[l - 1];
+        w.idun()[l] = 1.0 / sqrt(a * a + b * b);
+    }
     if (with_state_rows) {
         for (int r = l; r < 2 * N; r += P) {
             double s = 0.0;
@@ -591,20 +617,32 @@ constexpr unsigned char kCandRow = 2;     // row of a failed warm-start candidat
 // rows are never materialised.
 struct StructRows {
     static constexpr bool kHasUnitRows = true;
-    int N, mode;  // mode: NTM_MODE_BOX or NTM_MODE_FULL (NONE: no rows)
-    double umin, umax, xmin0, xmin1, xmax0, xmax1;
+    int N, mode;  // NTM_MODE_BOX, NTM_MODE_FULL or NTM_MODE_FULL_DU (NONE: no rows)
+    double umin, umax, xmin0, xmin1, xmax0, xmax1, du;
 
     __device__ __forceinline__ StructRows(const Prob& p)
         : N(p.N), mode(p.mode), umin(p.umin), umax(p.umax), xmin0(p.xmin[0]), xmin1(p.xmin[1]),
-          xmax0(p.xmax[0]), xmax1(p.xmax[1]) {}
+          xmax0(p.xmax[0]), xmax1(p.xmax[1]), du(p.du) {}
+    __device__ __forceinline__ bool has_state() const { return mode >= NTM_MODE_FULL; }
+    __device__ __forceinline__ bool has_rate() const { return mode == NTM_MODE_FULL_DU; }
     __device__ __forceinline__ double xmin(int c) const { return c ? xmin1 : xmin0; }
     __device__ __forceinline__ double xmax(int c) const { return c ? xmax1 : xmax0; }
 
-    __device__ __forceinline__ int rows() const { return mode == NTM_MODE_BOX ? 2 * N : 6 * N + 4; }
+    __device__ __forceinline__ int rows() const {
+        return mode == NTM_MODE_NONE ? 0 : (mode == NTM_MODE_BOX ? 2 * N : (mode == NTM_MODE_FULL_DU ? 8 * N + 2 : 6 * N + 4));
+    }
 
-    // decode a row id: kind 0 = u lower, 1 = u upper, 2 = state min, 3 = state max;
-    // j = variable (u rows) or state row r (state rows); -1 for x_0 rows
+    // decode a row id: kind 0 = u lower, 1 = u upper, 2 = state min, 3 = state max,
+    // 4 = rate up (U_j - U_{j-1} <= du), 5 = rate down (U_{j-1} - U_j <= du);
+    // j = variable (u and rate rows) or state row r (state rows); -1 for x_0 rows.
+    // Rate rows follow the 6N+4 getWLc rows: id = 6N+4 + 2(j-1) + {0 up, 1 down}.
     __device__ __forceinline__ void decode(int id, int N, int& kind, int& j) const {
+        if (mode == NTM_MODE_FULL_DU && id >= 6 * N + 4) {
+            const int t = id - (6 * N + 4);
+            kind = 4 + (t & 1);
+            j = (t >> 1) + 1;
+            return;
+        }
         if (mode == NTM_MODE_BOX) {
             kind = id < N ? 0 : 1;
             j = id < N ? id : id - N;
@@ -631,6 +669,10 @@ struct StructRows {
         int kind, j;
         decode(id, w.n(), kind, j);
         if (kind < 2) return (col == j) ? (kind == 0 ? -1.0 : 1.0) : 0.0;
+        if (kind >= 4) {
+            const double sg = kind == 4 ? 1.0 : -1.0;
+            return col == j ? sg : (col == j - 1 ? -sg : 0.0);
+        }
         if (j < 0 || col > (j >> 1)) return 0.0;
         double g = w.gt(j, col);
         return kind == 2 ? -g : g;
@@ -641,6 +683,7 @@ struct StructRows {
         decode(id, w.n(), kind, j);
         if (kind == 0) return -umin;
         if (kind == 1) return umax;
+        if (kind >= 4) return du;
         int c = j & 1;
         return kind == 2 ? (-xmin(c) + w.e()[j]) : (xmax(c) - w.e()[j]);
     }
@@ -648,6 +691,7 @@ struct StructRows {
     __device__ __forceinline__ double rnorm(const W& w, int id) const {
         int kind, j;
         decode(id, w.n(), kind, j);
+        if (kind >= 4) return 1.0 / w.idun()[j];
         return kind < 2 ? w.D()[j] : w.rn()[j];
     }
 
@@ -655,7 +699,7 @@ struct StructRows {
     template <int P, class W>
     __device__ __forceinline__ bool feasible_const(const W& w, double x0, double x1, int l) const {
         int bad = 0;
-        if (mode == NTM_MODE_FULL) {
+        if (has_state()) {
             if (l == 0) {
                 bad |= (x0 - xmin(0)) < 0.0;
                 bad |= (x1 - xmin(1)) < 0.0;
@@ -700,7 +744,14 @@ struct StructRows {
             consider(Vl - lo, idl, lo);
             consider(hi - Vl, idh, -hi);
         }
-        if (mode == NTM_MODE_FULL) {
+        if (has_rate() && l >= 1 && l < N) {                 // rate rows on lane j
+            const double ir = w.idun()[l];
+            const double dU = w.U()[l] - w.U()[l - 1];
+            const int id0 = 6 * N + 4 + 2 * (l - 1);
+            consider((du - dU) * ir, id0, -(du * ir));
+            consider((du + dU) * ir, id0 + 1, -(du * ir));
+        }
+        if (has_state()) {
             for (int r = l; r < 2 * N; r += P) {
                 double ir = w.irn()[r];
                 if (ir > 0.0) {
@@ -921,6 +972,7 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
         Pick pk = rows.template check<P>(w, Vl, l, false, fmax(1.0, vmax));
         NTM_ACC(ST_GI_CHECK, tg);
         NTM_CNT(CN_CHECK);
+        NTM_TRACE("GI it %d q %d pick %d s %.6e bc %.6e\n", it, q, pk.p, pk.s, pk.bc);
         if (pk.p < 0 || pk.s >= -1e-12 * fmax(fmax(1.0, vmax), fabs(pk.bc))) {
             *iters_out = it;
             *q_out = q;
@@ -971,6 +1023,7 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
             double dnrm = gsum<P>(dl * dl);
             double t2 = (zn <= 1e-300 || zn <= (kDepTol * kDepTol) * dnrm) ? kInf : -sp / zn;
             double t = fmin(t1, t2);
+            NTM_TRACE("   dir: t1 %.6e (pos %d) t2 %.6e zn %.6e dn %.6e sp %.6e\n", t1, li, t2, zn, dnrm, sp);
             NTM_ACC(ST_GI_DIR, tg);
             if (!(t < kInf)) { *iters_out = it; *q_out = q; return NTM_EXIT_INFEASIBLE; }
             if (l < q) w.uu()[l] = fmax(0.0, w.uu()[l] - t * rl);
@@ -1305,6 +1358,10 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
             double lv = kind == 0 ? -1.0 : 1.0;
             ufix = rows.bval(w, id) / lv;
             nfix = -((lv * w.D()[j]) / w.D()[j]);
+        } else if (kind >= 4) {                           // rate row: Lin = sg (e_j - e_{j-1})
+            isgen = 1;
+            srow = 2 * N + j;                             // general-row code >= 2N: rate row j
+            ssign = (kind == 4) ? 1.0 : -1.0;
         } else {                                          // state row r = j: Lin = -+Gamma_r
             const double sg = (kind == 2) ? -1.0 : 1.0;
             const int jm = j >> 1;
@@ -1410,6 +1467,12 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
     // GI normal of general row s at variable j: n = -(Lin_j D_j)/rn, Lin = sg Gamma_r
     auto gen_n = [&](int s2, int j) -> double {
         const int r = w.srw()[s2];
+        if (r >= 2 * N) {                                 // rate row i = r - 2N
+            const int i = r - 2 * N;
+            const double sg = w.ssg()[s2];
+            const double lv = (j == i) ? sg : (j == i - 1 ? -sg : 0.0);
+            return -((lv * w.D()[j]) * w.idun()[i]);
+        }
         return (j <= (r >> 1)) ? -(((w.ssg()[s2] * w.gt(r, j)) * w.D()[j]) * w.irn()[r]) : 0.0;
     };
     NTM_ACC(ST_P_GRAM, tp);
@@ -1431,10 +1494,19 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
             double hs = 0.0;
             if (l < nS) {
                 const int r = w.srw()[l];
-                const int c = r & 1;
-                const double sg = w.ssg()[l], ir = w.irn()[r];
-                const double bval = (sg > 0.0) ? (rows.xmax(c) - w.e()[r]) : (-rows.xmin(c) + w.e()[r]);
-                hs = -(bval * ir) + (sg * w.Phi()[r]) * ir;
+                const double sg = w.ssg()[l];
+                if (r >= 2 * N) {                         // rate row i: b = du, fixed part sg (U_i - U_{i-1})
+                    const int i = r - 2 * N;
+                    const double ir = w.idun()[i];
+                    const double ui = w.fx()[i] ? w.Uf()[i] : 0.0;
+                    const double um = w.fx()[i - 1] ? w.Uf()[i - 1] : 0.0;
+                    hs = -(rows.du * ir) + (sg * (ui - um)) * ir;
+                } else {
+                    const int c = r & 1;
+                    const double ir = w.irn()[r];
+                    const double bval = (sg > 0.0) ? (rows.xmax(c) - w.e()[r]) : (-rows.xmin(c) + w.e()[r]);
+                    hs = -(bval * ir) + (sg * w.Phi()[r]) * ir;
+                }
             }
             NTM_WSYNC();
             if (l < nS) {                          // Y = L^{-1} E': lane s solves column s
@@ -1616,7 +1688,7 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
     free_response<P>(w, x0, x1, l);
     f_phase<P>(pb, w, l);
     NTM_ACC(ST_COST, tq);
-    const bool full = pb.mode == NTM_MODE_FULL;
+    const bool full = pb.mode >= NTM_MODE_FULL;        // state rows present
     int flag, q = 0, ns = 0;
     *qp_iters = 0;
     StructRows rows(pb);
@@ -1652,7 +1724,9 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                     if (n_try) ++*n_try;
                     int fk = 0, fp = 0;
                     double vf = 0.0;
-                    if (polish_compact<P>(pb, w, rows, cq, l, true, &ns, &fk, &fp, &vf)) {
+                    const bool okc = polish_compact<P>(pb, w, rows, cq, l, true, &ns, &fk, &fp, &vf);
+                    NTM_TRACE("QP cand rep %d cq %d ok %d fk %d fp %d\n", rep, cq, (int)okc, fk, fp);
+                    if (okc) {
                         flag = NTM_EXIT_OPTIMAL;
                         q = cq;
                         done = true;
@@ -1702,7 +1776,11 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                     flag = gi_solve<P, StructRows, W>(w, rows, pb.mode != NTM_MODE_NONE, nrows, l,
                                                       qp_iters, &q);
                     NTM_ACC(ST_GI, tq);
-                    if (flag == NTM_EXIT_OPTIMAL) (void)polish_compact<P>(pb, w, rows, q, l, false, &ns);
+                    if (flag == NTM_EXIT_OPTIMAL) {
+                        const bool okp = polish_compact<P>(pb, w, rows, q, l, false, &ns);
+                        NTM_TRACE("QP GI flag %d q %d polish %d\n", flag, q, (int)okp);
+                        (void)okp;
+                    }
                     NTM_ACC(ST_POLISH, tq);
                 }
             }

@@ -54,7 +54,7 @@ __device__ __forceinline__ int64_t xcd_swizzle(int64_t b, int64_t nb) {
 template <int P, class W>
 __device__ void load_candidates(const Prob& pb, const W& w, int64_t B, int64_t s, const int32_t* ws, int l) {
     const int N = w.n();
-    const int nrows = pb.mode == NTM_MODE_BOX ? 2 * N : (pb.mode == NTM_MODE_FULL ? 6 * N + 4 : 0);
+    const int nrows = StructRows(pb).rows();
     for (int e = l; e < 2 * (N + 1); e += P) w.cand()[e] = ws[(int64_t)e * B + s];
     for (int i = l; i < nrows; i += P) w.aflag()[i] = 0;
     NTM_WSYNC();
@@ -83,7 +83,7 @@ __device__ void load_candidates(const Prob& pb, const W& w, int64_t B, int64_t s
 
 // one MPC step on LDS-resident state; returns exit flag, sets *iters
 template <int P, class W>
-__device__ int mpc_step_dev(const Prob& pb, const W& w, double x0, double x1, int l, int* iters,
+__device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x0, double x1, int l, int* iters,
                             int64_t B = 0, int64_t s = 0) {
     int flag = NTM_EXIT_OPTIMAL, it;
     int n_qp = 0, n_gi = 0, n_act = 0, n_gen = 0, n_try = 0, n_girun = 0;
@@ -126,6 +126,7 @@ __global__ __launch_bounds__(64, NTM_HOT_WAVES_PER_EU) void k_mpc_step(Prob pb, 
     const int64_t s = xcd_swizzle(blockIdx.x, gridDim.x) * G + g;
     const int N = NN > 0 ? NN : pb.N;
     NTM_STAMPS_INIT();
+    NTM_TRACE_SET(s, g, l);
     if (s >= B) return;
     auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
     const double x0 = x_k[s], x1 = x_k[B + s];
@@ -404,6 +405,7 @@ Prob make_prob(const ntm_physics* p, const ntm_config* c) {
     pb.i_sim = c->i_sim;
     pb.mode = c->mode;
     pb.flags = c->flags;
+    pb.du = c->du_max;
     for (int i = 0; i < 2; ++i) {
         pb.xmin[i] = c->xmin[i];
         pb.xmax[i] = c->xmax[i];
@@ -460,7 +462,9 @@ int validate(ntm_ctx* ctx, const ntm_physics* p, const ntm_config* c, int64_t B)
     if (!p || !c) return fail(ctx, NTM_E_INVALID, "null physics/config");
     if (c->N < 1 || c->N > NTM_MAX_N) return fail(ctx, NTM_E_INVALID, "N out of range [1, 64]");
     if (c->i_sim < 1) return fail(ctx, NTM_E_INVALID, "i_sim must be >= 1");
-    if (c->mode < NTM_MODE_NONE || c->mode > NTM_MODE_FULL) return fail(ctx, NTM_E_INVALID, "bad mode");
+    if (c->mode < NTM_MODE_NONE || c->mode > NTM_MODE_FULL_DU) return fail(ctx, NTM_E_INVALID, "bad mode");
+    if (c->mode == NTM_MODE_FULL_DU && !(std::isfinite(c->du_max)))
+        return fail(ctx, NTM_E_INVALID, "du_max must be finite");
     if (B < 0) return fail(ctx, NTM_E_INVALID, "negative batch");
     return NTM_OK;
 }
@@ -582,6 +586,7 @@ void ntm_config_default(ntm_config* c, int32_t N) {
     c->r[0] = 0;
     c->r[1] = 1000 * 2 * pi;
     c->epsilon = 1e-14;
+    c->du_max = 5e5;   // config 5 only (not in the reference): a quarter of the input range per step
 }
 
 int32_t ntm_abi_version(void) { return NTM_MPC_ABI_VERSION; }

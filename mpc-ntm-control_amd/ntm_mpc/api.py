@@ -77,16 +77,21 @@ class Config:
     epsilon: float = 1e-14
     mode: int = L.MODE_FULL
     flags: int = 0
+    du_max: float = 5e5      # NTM_MODE_FULL_DU (config 5, extension): |U_i - U_{i-1}| <= du_max
 
     def to_c(self) -> NtmConfig:
         return NtmConfig(int(self.N), int(self.i_sim), int(self.mode), int(self.flags), float(self.Ts),
                          (C.c_double * 2)(*self.xmin), (C.c_double * 2)(*self.xmax), float(self.umin),
                          float(self.umax), (C.c_double * 4)(*self.Q), (C.c_double * 2)(*self.r),
-                         float(self.epsilon))
+                         float(self.epsilon), float(self.du_max))
 
     @property
     def m(self) -> int:
-        return 0 if self.mode == L.MODE_NONE else (2 * self.N if self.mode == L.MODE_BOX else 6 * self.N + 4)
+        if self.mode == L.MODE_NONE:
+            return 0
+        if self.mode == L.MODE_BOX:
+            return 2 * self.N
+        return 6 * self.N + 4 + (2 * (self.N - 1) if self.mode == L.MODE_FULL_DU else 0)
 
 
 def _ptr(t: torch.Tensor | None):

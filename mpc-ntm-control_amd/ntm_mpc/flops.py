@@ -19,7 +19,7 @@ K = GI iterations (all per MPC step), q / s = final active rows / general
 """
 from __future__ import annotations
 
-MODE_NONE, MODE_BOX, MODE_FULL = 0, 1, 2
+MODE_NONE, MODE_BOX, MODE_FULL, MODE_FULL_DU = 0, 1, 2, 3
 
 
 def common_build(N: int, mode: int) -> float:
@@ -28,8 +28,10 @@ def common_build(N: int, mode: int) -> float:
     f += 8 * N                                        # e = Phi x_k + Lambda
     f += 10 * N + 2 * N * (N + 1)                     # F~ = D 2 Gamma' Om (e - r)
     f += 5 * N * (N + 1) + 4 * N                      # diag(G~) -> D, scaled bounds
-    if mode == MODE_FULL:
+    if mode >= MODE_FULL:
         f += 3 * N * (N + 1) + 2 * N                  # state-row norms |Gamma_r D|
+    if mode == MODE_FULL_DU:
+        f += 4 * (N - 1)                              # rate-row norms
     return f
 
 
@@ -38,8 +40,10 @@ def check(N: int, mode: int) -> float:
     if mode == MODE_NONE:
         return 0.0
     f = 2 * N                                         # u bounds
-    if mode == MODE_FULL:
+    if mode >= MODE_FULL:
         f += 2 * N * (N + 1) + 8 * N                  # x^ = Gamma U + e, two slacks per state row
+    if mode == MODE_FULL_DU:
+        f += 5 * (N - 1)                              # U_i - U_{i-1}, two slacks per rate pair
     return f
 
 
@@ -79,7 +83,7 @@ def per_step(N: int, mode: int, qps: float, tries: float, giruns: float, K: floa
              s: float) -> float:
     """Useful fp64 flops of one MPC step (one scenario k -> k+1)."""
     qbar = q / 2.0
-    state_frac = (s / q) if (mode == MODE_FULL and q > 0) else 0.0
+    state_frac = (s / q) if (mode >= MODE_FULL and q > 0) else 0.0
     f = qps * (common_build(N, mode) + rollout(N))
     f += (tries + giruns) * polish(N, mode, q, s)
     f += giruns * (gi_setup(N) + check(N, mode))

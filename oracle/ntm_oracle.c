@@ -31,7 +31,7 @@
 #include "../include/ntm_mpc.h"
 
 #define NMAX NTM_MAX_N
-#define MMAX (6 * NMAX + 4)
+#define MMAX (8 * NMAX + 4)   /* getWLc rows + rate rows (NTM_MODE_FULL_DU) */
 
 typedef struct {
     double a11c, a21num_den, a22, bc, C1, C2, wmarg2, wdep;
@@ -553,6 +553,23 @@ static int orc_solve(const orc_coef* k, const ntm_config* c, const double* rho,
     double W[MMAX * 2], L[MMAX * NMAX], cv[MMAX];
     orc_getwlc(c, Phi, Gam, Lam, W, L, cv);
     for (int i = 0; i < m; ++i) cv[i] += W[i] * x[0] + W[m + i] * x[1];   /* c + W x_k (:97) */
+    if (c->mode == NTM_MODE_FULL_DU) {
+        /* config 5 (extension): rate rows after the getWLc rows; L is col-major m x N,
+         * so re-stride it to mm = m + 2(N-1) rows */
+        int mm = m + 2 * (N - 1);
+        double L2[MMAX * NMAX];
+        memset(L2, 0, sizeof(double) * (size_t)mm * N);
+        for (int j = 0; j < N; ++j)
+            for (int i = 0; i < m; ++i) L2[(size_t)j * mm + i] = L[(size_t)j * m + i];
+        for (int i = 1; i < N; ++i) {
+            int r = m + 2 * (i - 1);
+            L2[(size_t)i * mm + r] = 1.0;       L2[(size_t)(i - 1) * mm + r] = -1.0;
+            L2[(size_t)i * mm + r + 1] = -1.0;  L2[(size_t)(i - 1) * mm + r + 1] = 1.0;
+            cv[r] = c->du_max;
+            cv[r + 1] = c->du_max;
+        }
+        return orc_qp(N, mm, G, F, L2, cv, U, qp_iters);
+    }
     return orc_qp(N, m, G, F, L, cv, U, qp_iters);
 }
 
@@ -602,7 +619,7 @@ static void orc_step(const orc_coef* k, const ntm_config* c, const double* x,
 #define EXPORT __attribute__((visibility("default")))
 
 static int valid(const ntm_config* c) {
-    return c && c->N >= 1 && c->N <= NMAX && c->i_sim >= 1 && c->mode >= 0 && c->mode <= 2;
+    return c && c->N >= 1 && c->N <= NMAX && c->i_sim >= 1 && c->mode >= 0 && c->mode <= 3;
 }
 
 EXPORT int ntm_oracle_rho(const ntm_physics* p, const ntm_config* c, const double* x, double* rho3) {

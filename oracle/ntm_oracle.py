@@ -74,6 +74,9 @@ class Physics:
 MODE_NONE = 0   # unconstrained LQ (BASELINE config 1)
 MODE_BOX = 1    # u in [umin, umax] only (BASELINE config 2)
 MODE_FULL = 2   # full getWLc.m polyhedron (BASELINE config 3/4)
+MODE_FULL_DU = 3  # getWLc rows + input-rate rows |U_i - U_{i-1}| <= du_max (BASELINE
+                  # config 5; an extension of getWLc.m's row structure, not in the
+                  # reference: parity for this mode is pinned only by this oracle)
 
 # flags
 LITERAL_PHI_RIGHTMUL = 1 << 0    # D4: Phi_j = Phi_{j-1} * A_j
@@ -98,6 +101,7 @@ class Config:
     epsilon: float = 1e-14                       # :87
     mode: int = MODE_FULL
     flags: int = 0
+    du_max: float = 5e5                          # MODE_FULL_DU only (W per step)
 
     @property
     def m_rows(self) -> int:
@@ -109,6 +113,8 @@ def constraint_rows(N: int, mode: int) -> int:
         return 0
     if mode == MODE_BOX:
         return 2 * N
+    if mode == MODE_FULL_DU:
+        return 8 * N + 2                          # getWLc rows + 2(N-1) rate rows
     return 6 * N + 4                              # getWLc.m:30-44
 
 
@@ -277,7 +283,20 @@ def constraints(Phi, Gamma, Lam, xk, cfg: Config):
         b = np.concatenate([np.full(N, -cfg.umin), np.full(N, cfg.umax)])
         return Lin, b
     W, L, c = getWLc(cfg.xmax, cfg.xmin, cfg.umax, cfg.umin, Gamma, Phi, Lam)
-    return L, c + W @ xk                                                                # NTM_MPC_Sim.m:97
+    Lin, b = L, c + W @ xk                                                              # NTM_MPC_Sim.m:97
+    if cfg.mode == MODE_FULL_DU:
+        Lin, b = np.vstack([Lin, rate_rows(N)]), np.concatenate([b, np.full(2 * (N - 1), cfg.du_max)])
+    return Lin, b
+
+
+def rate_rows(N):
+    """Input-rate rows appended after getWLc's 6N+4 (config 5): for i = 1..N-1,
+    row 2(i-1):  U_i - U_{i-1} <= du_max;  row 2(i-1)+1:  U_{i-1} - U_i <= du_max."""
+    R = np.zeros((2 * (N - 1), N))
+    for i in range(1, N):
+        R[2 * (i - 1), i], R[2 * (i - 1), i - 1] = 1.0, -1.0
+        R[2 * (i - 1) + 1, i], R[2 * (i - 1) + 1, i - 1] = -1.0, 1.0
+    return R
 
 # --------------------------------------------------------------------------
 # L2'': QP  (quadprog call site NTM_MPC_Sim.m:97; exitflag :98-103)

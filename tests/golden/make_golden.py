@@ -82,6 +82,9 @@ def main():
     closed_loop_fixture(20, O.MODE_FULL, [0, 1, 2], 6)      # config 3 shape
     qp_fixture(20, O.MODE_FULL, 12)
     qp_fixture(20, O.MODE_BOX, 8)
+    # BASELINE config 5 row structure (input-rate rows, an extension of getWLc)
+    closed_loop_fixture(20, O.MODE_FULL_DU, [0, 1], 6)
+    qp_fixture(20, O.MODE_FULL_DU, 8)
     print("fixtures written to", HERE)
 
 

@@ -23,6 +23,11 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda:0"
 U_TOL = 1e-10
+# mode 3 (BASELINE config 5, input-rate rows: an extension, not in the reference):
+# the rate rows make the active KKT systems ill-conditioned; the two fp64 CPU
+# restatements differ by up to 8.4e-9 umax and each sits within ~4e-9 umax of a
+# 30-digit solve of the same active set, so the per-step bound is 5e-8 umax
+U_TOL_RATE = 5e-8
 
 
 def T(a):
@@ -156,7 +161,7 @@ def _qp_batch(N, mode, B, seed):
     return Gs, Fs, Ls, bs
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 def test_quadprog_matches_oracle(ctl, mode):
     N, B = 20, 24
     Gs, Fs, Ls, bs = _qp_batch(N, mode, B, 100)
@@ -171,17 +176,27 @@ def test_quadprog_matches_oracle(ctl, mode):
         Ur, fr, _ = cbind.qp(Gs[s], Fs[s], Ls[s] if m else None, bs[s] if m else None)
         assert flag[s] == fr
         scale = max(2e6, np.max(np.abs(Ur)))       # mode 0 minimisers are unbounded (~1e11)
-        assert np.max(np.abs(U[:, s] - Ur)) / scale <= U_TOL, (s, np.max(np.abs(U[:, s] - Ur)))
+        tol = U_TOL_RATE if mode == 3 else U_TOL
+        assert np.max(np.abs(U[:, s] - Ur)) / scale <= tol, (s, np.max(np.abs(U[:, s] - Ur)))
 
 
 # ---------------------------------------------------------------- a7, a12, a13: one MPC step
 @pytest.mark.parametrize("N,mode,warm", [(10, 0, False), (20, 1, False), (20, 2, False), (3, 2, False),
                                          (50, 2, False), (50, 1, False), (20, 2, True), (20, 1, True),
-                                         (50, 2, True)])
+                                         (50, 2, True), (20, 3, False), (20, 3, True), (4, 3, False),
+                                         (50, 3, True)])
 def test_step_teacher_forced(ctl, N, mode, warm):
     """Each step, the GPU and the oracle get identical (x_k, rho, U_old); with
     warm=True the GPU also carries its active-set workspace from step to step
-    (ntm_mpc_step_ws_device), which must not change the answer."""
+    (ntm_mpc_step_ws_device), which must not change the answer.
+
+    The LPV loop stops on sum|U - Uold| < 1e-14 (NTM_MPC_Sim.m:123, D14), i.e. on
+    a bitwise fixed point, so GPU and CPU rounding may stop it one iteration
+    apart.  In modes 0-2 the loop is contractive and every scenario still
+    agrees; with input-rate rows (mode 3) the loop can 2-cycle between active
+    sets, and a scenario whose path diverged (different inner-iteration count,
+    DESIGN.md §3) legitimately ends elsewhere: there only the scenarios that
+    took the same path are compared, and >= 90% of them must."""
     B, k_sim = 48, 12 if N < 50 else 4
     cfg, ocfg = cfgs(N, mode)
     x = O.scenario_x0(np.arange(B)).T if mode else np.tile(O.REFERENCE_X0[:, None], (1, B))
@@ -194,19 +209,48 @@ def test_step_teacher_forced(ctl, N, mode, warm):
         tr, tu = T(rho), T(Uo)
         out = ctl.step(T(x), tr, tu, cfg, active_ws=ws)
         assert (H(out["exitflag"]) == ref["exitflag"]).all(), k
-        # the LPV loop stops on sum|U - Uold| < 1e-14 (NTM_MPC_Sim.m:123), i.e. on a
-        # bitwise fixed point: GPU and CPU rounding may reach it one iteration apart
-        same_iters += int((H(out["inner_iters"]) == ref["inner_iters"]).sum())
+        same = H(out["inner_iters"]) == ref["inner_iters"]
+        same_iters += int(same.sum())
         n += x.shape[1]
-        worst = max(worst, np.max(np.abs(H(out["U"]) - ref["U"])) / cfg.umax)
+        cmp = same if mode == 3 else np.ones_like(same)
+        worst = max(worst, np.max(np.abs(H(out["U"]) - ref["U"])[:, cmp], initial=0.0) / cfg.umax)
         xn = H(out["x_next"])
-        assert np.max(np.abs(xn - ref["x_next"]) / xscale) <= 1e-9
+        assert np.max(np.abs(xn - ref["x_next"])[:, cmp] / xscale, initial=0.0) <= 1e-9
         xp = H(out["x_pred"]).reshape(N + 1, 2, -1).transpose(1, 0, 2)
         xr = ref["x_pred"].reshape(N + 1, 2, -1).transpose(1, 0, 2)
-        assert np.max(np.abs(xp - xr) / xscale[:, :, None]) <= 1e-9
+        assert np.max(np.abs(xp - xr)[:, :, cmp] / xscale[:, :, None], initial=0.0) <= 1e-9
         x, rho, Uo = ref["x_next"], ref["rho"], ref["U_old"]
-    assert worst <= (U_TOL if N <= 20 else 1e-8), worst
+    assert worst <= (U_TOL_RATE if mode == 3 else (U_TOL if N <= 20 else 1e-8)), worst
     assert same_iters >= 0.9 * n, (same_iters, n)
+
+
+@pytest.mark.parametrize("N", [4, 20])
+def test_rate_qps_match_oracle(ctl, N):
+    """Mode 3's QPs themselves (not the LPV path): every QP the oracle meets
+    along its trajectory, solved through ntm_qp_device, matches the oracle."""
+    B, k_sim = 16, 6
+    _, ocfg = cfgs(N, 3)
+    ph = O.Physics()
+    x = O.scenario_x0(np.arange(B)).T.copy()
+    rho, Uo = cbind.initial_state(x, ocfg)
+    Gs, Fs, Ls, bs = [], [], [], []
+    for k in range(k_sim):
+        for s in range(B):
+            Rho = rho[:, s].reshape(N, 3).T
+            Phi, Gam, Lam = O.lift(Rho, ph, ocfg)
+            G, F = O.cost(Phi, Gam, Lam, x[:, s], ocfg)
+            Lin, b = O.constraints(Phi, Gam, Lam, x[:, s], ocfg)
+            Gs.append(G), Fs.append(F), Ls.append(Lin), bs.append(b)
+        ref = cbind.step(x, rho, Uo, ocfg)
+        x, rho, Uo = ref["x_next"], ref["rho"], ref["U_old"]
+    Gb = np.stack([g.reshape(-1, order="F") for g in Gs], axis=1)
+    Lb = np.stack([l_.reshape(-1, order="F") for l_ in Ls], axis=1)
+    U, flag, _ = ctl.quadprog(T(Gb), T(np.stack(Fs, axis=1)), T(Lb), T(np.stack(bs, axis=1)))
+    U, flag = H(U), H(flag)
+    for i in range(len(Gs)):
+        Ur, fr, _ = cbind.qp(Gs[i], Fs[i], Ls[i], bs[i])
+        assert flag[i] == fr
+        assert np.max(np.abs(U[:, i] - Ur)) / 2e6 <= U_TOL_RATE, i
 
 
 def test_step_reference_x0_infeasible(ctl):
@@ -244,7 +288,7 @@ def test_step_ragged_batches(ctl, B):
 
 
 # ---------------------------------------------------------------- closed loop
-@pytest.mark.parametrize("N,mode", [(10, 0), (20, 1), (20, 2)])
+@pytest.mark.parametrize("N,mode", [(10, 0), (20, 1), (20, 2), (20, 3)])
 def test_run_closed_loop(ctl, N, mode):
     B, k_sim = 32, 20
     cfg, ocfg = cfgs(N, mode)

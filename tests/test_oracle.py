@@ -196,7 +196,7 @@ def test_qp_matches_active_set_enumeration():
 def test_qp_golden_certified():
     """Committed QPs (N=20) with 50-digit-certified optima: the oracle's fp64
     solution is within 1e-11 * umax of the exact KKT point."""
-    for name in ("qp_m2_N20.npz", "qp_m1_N20.npz"):
+    for name in ("qp_m2_N20.npz", "qp_m1_N20.npz", "qp_m3_N20.npz"):
         d = np.load(GOLD / name)
         for i in range(d["G"].shape[0]):
             U, flag, info = O.qp_solve(d["G"][i], d["F"][i], d["Lin"][i], d["b"][i])
@@ -232,7 +232,37 @@ def test_unconstrained_lq_vs_mpmath():
 
 
 # ------------------------------------------------------------------ closed loop
-@pytest.mark.parametrize("name", ["closed_loop_m0_N10.npz", "closed_loop_m2_N3.npz"])
+def test_rate_rows_structure():
+    """Config 5 rows (extension): after getWLc's 6N+4 rows, pairs
+    U_i - U_{i-1} <= du and U_{i-1} - U_i <= du for i = 1..N-1."""
+    N = 5
+    c = cfg(N, O.MODE_FULL_DU)
+    assert c.m_rows == 8 * N + 2 == O.constraint_rows(N, O.MODE_FULL_DU)
+    Rho = O.initial_rho(O.scenario_x0([3])[0], PH, c)
+    Phi, Gam, Lam = O.lift(Rho, PH, c)
+    Lin, b = O.constraints(Phi, Gam, Lam, O.scenario_x0([3])[0], c)
+    L2, b2 = O.constraints(Phi, Gam, Lam, O.scenario_x0([3])[0], cfg(N, O.MODE_FULL))
+    np.testing.assert_array_equal(Lin[:6 * N + 4], L2)
+    np.testing.assert_array_equal(b[:6 * N + 4], b2)
+    U = np.array([1.0, 4.0, 2.0, 2.0, 7.0])
+    dU = np.diff(U)
+    np.testing.assert_array_equal(Lin[6 * N + 4::2] @ U, dU)
+    np.testing.assert_array_equal(Lin[6 * N + 5::2] @ U, -dU)
+    assert np.all(b[6 * N + 4:] == c.du_max)
+
+
+def test_rate_limited_closed_loop_respects_rows():
+    """Every applied plan of the mode-3 closed-loop fixture satisfies the rate
+    rows and the input box (to rounding), and the rate rows do bind."""
+    d = np.load(GOLD / "closed_loop_m3_N20.npz")
+    c = cfg(20, O.MODE_FULL_DU)
+    Uk = d["Uk"]                                        # (scenarios, N, k_sim)
+    assert np.max(np.abs(np.diff(Uk, axis=1))) <= c.du_max * (1 + 1e-9)
+    assert np.max(np.abs(np.diff(Uk, axis=1))) >= c.du_max * (1 - 1e-9)
+    assert Uk.min() >= c.umin - 1e-9 * c.umax and Uk.max() <= c.umax * (1 + 1e-12)
+
+
+@pytest.mark.parametrize("name", ["closed_loop_m0_N10.npz", "closed_loop_m2_N3.npz", "closed_loop_m3_N20.npz"])
 def test_closed_loop_golden(name):
     """Regression pin: the oracle reproduces its committed closed-loop fixtures."""
     d = np.load(GOLD / name)

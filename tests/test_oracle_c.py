@@ -36,7 +36,7 @@ def test_c_functions_match_python(N):
     np.testing.assert_allclose(cv, d["c"], rtol=1e-14, atol=1e-15)
 
 
-@pytest.mark.parametrize("name", ["qp_m2_N20.npz", "qp_m1_N20.npz"])
+@pytest.mark.parametrize("name", ["qp_m2_N20.npz", "qp_m1_N20.npz", "qp_m3_N20.npz"])
 def test_c_qp_matches_certified(name):
     d = np.load(f"tests/golden/{name}")
     for i in range(d["G"].shape[0]):
@@ -45,7 +45,7 @@ def test_c_qp_matches_certified(name):
         assert np.max(np.abs(U - d["U_exact"][i])) / 2e6 <= 1e-11
 
 
-@pytest.mark.parametrize("N,mode", [(10, 0), (3, 2), (20, 1), (20, 2)])
+@pytest.mark.parametrize("N,mode", [(10, 0), (3, 2), (20, 1), (20, 2), (20, 3), (4, 3)])
 def test_c_step_teacher_forced(N, mode):
     """Per-step agreement (identical inputs every step) of the two oracles."""
     c = O.Config(N=N, mode=mode)
@@ -57,12 +57,17 @@ def test_c_step_teacher_forced(N, mode):
         for s in range(B):
             out = O.mpc_step(x[:, s], rho[:, s].reshape(N, 3).T, Uo[:, s], PH, c)
             assert out["exitflag"] == ref["exitflag"][s]
-            assert np.max(np.abs(out["U"] - ref["U"][:, s])) <= 1e-10 * max(c.umax, np.max(np.abs(out["U"])))
+            # mode 3 (config 5 extension): with rate rows the active KKT systems are
+            # ill-conditioned (cond(G) ~ 1e11); both fp64 restatements sit within
+            # ~4e-9 umax of a 30-digit solve of the same active set
+            tol = 5e-8 if mode == 3 else 1e-10
+            assert np.max(np.abs(out["U"] - ref["U"][:, s])) <= tol * max(c.umax, np.max(np.abs(out["U"])))
             np.testing.assert_allclose(out["xnext"], ref["x_next"][:, s], rtol=1e-10, atol=1e-15)
         x, rho, Uo = ref["x_next"], ref["rho"], ref["U_old"]
 
 
 @pytest.mark.parametrize("name", ["closed_loop_m1_N20.npz", "closed_loop_m2_N20.npz", "closed_loop_m2_N3.npz",
+                                  "closed_loop_m3_N20.npz",
                                   "closed_loop_m0_N10.npz"])
 def test_c_closed_loop_vs_golden(name):
     d = np.load(f"tests/golden/{name}")
