@@ -100,6 +100,7 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        ST_GI_DIR, ST_GI_ADD, ST_GI_DROP, CN_CHECK, CN_CAND, CN_HIT,
        ST_P_CLASS, ST_P_GRAM, ST_P_CHOL, ST_P_SCHUR, ST_P_BWD, ST_P_KKT, CN_REPAIR, CN_GIRUN };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
+constexpr int kMaxNT = 32;         // explicit R^{-1} in GI up to this horizon (WS::useT)
 constexpr int kRepairs = 8;        // single-row repairs of a failed warm-start candidate
 
 #define NTM_WSYNC()                                              \
@@ -291,8 +292,11 @@ struct WS {
     // double offsets of each array (n() is launch-uniform, so these fold to scalar math)
     __device__ __forceinline__ int oJ() const { return 14 * n() + n() * (n() + 1); }
     __device__ __forceinline__ int oR() const { return oJ() + n() * ldj(); }
+    // T = R^{-1} is kept for N <= kMaxNT only: at long horizons its N^2 doubles would
+    // halve the scenarios per CU, and the dual direction falls back to back substitution
+    __device__ __forceinline__ bool useT() const { return n() <= kMaxNT; }
     __device__ __forceinline__ int oT() const { return oR() + (n() + 1) * ldj(); }
-    __device__ __forceinline__ int oV() const { return oT() + n() * ldj(); }         // start of the vector block
+    __device__ __forceinline__ int oV() const { return oT() + (useT() ? n() * ldj() : 0); }   // vector block
     __device__ __forceinline__ double* rho() const { return base; }                 // 3N (3xN col-major)
     __device__ __forceinline__ double* a11() const { return base + 3 * n(); }         // n()
     __device__ __forceinline__ double* a21() const { return base + 4 * n(); }         // n()
@@ -346,7 +350,7 @@ struct WS {
 
 __host__ __device__ inline int ldj_of(int N) { return N | 1; }
 __host__ __device__ inline int ws_doubles(int N) {
-    return 14 * N + N * (N + 1) + 2 * N * ldj_of(N) + (N + 1) * ldj_of(N) + 24 * N + 3;
+    return 14 * N + N * (N + 1) + (N <= kMaxNT ? 2 : 1) * N * ldj_of(N) + (N + 1) * ldj_of(N) + 24 * N + 3;
 }
 __host__ __device__ inline int ws_bytes(int N) {
     int b = ws_doubles(N) * 8 + 6 * (N + 1) * 4 + N + (8 * N + 4);   // ..., fx (N), aflag (rows <= 8N+2)
@@ -964,7 +968,8 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
     }
     NTM_ACC(ST_GI_FACT, tg);
     if (!has_rows) return NTM_EXIT_OPTIMAL;
-    if (l < N) for (int b = 0; b < N; ++b) w.T()[l * LDJ + b] = 0.0;
+    const bool useT = w.useT();
+    if (useT && l < N) for (int b = 0; b < N; ++b) w.T()[l * LDJ + b] = 0.0;
     const int max_iter = 10 * (N + nrows) + 50;
     int q = 0, it = 0;
     for (;;) {
@@ -1006,8 +1011,18 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
             if (l < N) {
 #pragma unroll 4
                 for (int k2 = 0; k2 < N; ++k2) zl += w.J()[l * LDJ + k2] * w.d()[k2];
+                if (useT) {
 #pragma unroll 4
-                for (int b = 0; b < N; ++b) rl += w.T()[l * LDJ + b] * w.dr()[b];
+                    for (int b = 0; b < N; ++b) rl += w.T()[l * LDJ + b] * w.dr()[b];
+                }
+            }
+            if (!useT) {                       // long horizons: back substitution on R
+                double acc = (l < q) ? dl : 0.0;
+                for (int b = q - 1; b >= 0; --b) {
+                    const double rb = gbcast<P>(acc, b) / w.R()[b + b * LD];
+                    if (l == b) rl = rb;
+                    if (l < b) acc -= w.R()[l + b * LD] * rb;
+                }
             }
             // partial (dual) step length t1
             double ratio = (l < q && rl > 0.0) ? w.uu()[l] / rl : kInf;
@@ -1052,10 +1067,13 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
                     }
                     // R gains column q = [d1; h]; T = R^{-1} gains column q = [-r/h; 1/h]
                     const double ih = 1.0 / h;
-                    if (l < q) { w.R()[l + q * LD] = dl; w.T()[l * LDJ + q] = -rl * ih; }
+                    if (l < q) {
+                        w.R()[l + q * LD] = dl;
+                        if (useT) w.T()[l * LDJ + q] = -rl * ih;
+                    }
                     if (l == q) {
                         w.R()[q + q * LD] = h;
-                        w.T()[q * LDJ + q] = ih;
+                        if (useT) w.T()[q * LDJ + q] = ih;
                         w.act()[q] = p;
                         w.aflag()[p] = kActiveRow;
                         w.uu()[q] = upq;
@@ -1100,7 +1118,7 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
                     w.J()[l * LDJ + j] = cc * j1 + ss * j2;
                     w.J()[l * LDJ + j + 1] = -ss * j1 + cc * j2;
                 }
-                if (l < q) {   // T <- T G_j' (the columns rotate like J's)
+                if (useT && l < q) {   // T <- T G_j' (the columns rotate like J's)
                     double t1v = w.T()[l * LDJ + j], t2v = w.T()[l * LDJ + j + 1];
                     w.T()[l * LDJ + j] = cc * t1v + ss * t2v;
                     w.T()[l * LDJ + j + 1] = -ss * t1v + cc * t2v;
@@ -1109,10 +1127,10 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
             }
             // R'^{-1} = (T Q) without row l0 and column q-1.  Lane c owns column c:
             // rows l0+1..q-1 move up one; the discarded column q-1 is cleared
-            if (l < q - 1) {
+            if (useT && l < q - 1) {
                 for (int a = l0; a < q - 1; ++a) w.T()[a * LDJ + l] = w.T()[(a + 1) * LDJ + l];
                 w.T()[(q - 1) * LDJ + l] = 0.0;
-            } else if (l == q - 1) {
+            } else if (useT && l == q - 1) {
                 for (int a = 0; a < q; ++a) w.T()[a * LDJ + l] = 0.0;
             }
             NTM_WSYNC();
