@@ -876,6 +876,17 @@ struct DenseRows {
 // ---------------------------------------------------------------------------
 // Element (i, j) of a small matrix lives at A[i*RS + j*CS] (col-major: RS = 1,
 // CS = LD; the polish's K is stored transposed: RS = LD, CS = 1).
+// 1/sqrt(x) for x > 0: v_rsq_f64 plus two Newton steps (full fp64 accuracy;
+// the pivots of the small Cholesky factorisations sit on their sequential
+// critical path, where the IEEE sqrt + division expansions cost ~25 dependent ops)
+__device__ __forceinline__ double rsqrt_nr(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    y = fma(y, fma(-h * y, y, 0.5), y);
+    y = fma(y, fma(-h * y, y, 0.5), y);
+    return y;
+}
+
 // left-looking Cholesky of the n x n lower triangle of A, in place; the
 // reciprocals of the diagonal go to rdiag[0..n) (the triangular solves then
 // multiply instead of divide); false if not PD
@@ -888,9 +899,9 @@ __device__ bool chol_inplace(double* A, int n, int RS, int CS, int l, double* rd
             for (int j = 0; j < k; ++j) s -= A[l * RS + j * CS] * A[k * RS + j * CS];
         }
         double dk = gbcast<P>(s, k);
-        if (!(dk > 0.0)) return false;
-        double lk = sqrt(dk);
-        double il = 1.0 / lk;
+        if (!(dk > 0.0) || !(dk < kInf)) return false;
+        const double il = rsqrt_nr(dk);
+        const double lk = dk * il;
         if (l > k && l < n) A[l * RS + k * CS] = s * il;
         if (l == k) { A[k * RS + k * CS] = lk; rdiag[k] = il; }
         NTM_WSYNC();
