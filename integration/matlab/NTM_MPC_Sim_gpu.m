@@ -37,9 +37,10 @@ switch mode
         exitflag = zeros(k_sim, B, 'int32'); iters = zeros(k_sim, B, 'int32');
         xk(:, 1, :) = reshape(x0, 2, 1, B);
         [Rho, Uold] = ntm_mpc_mex('init', X0, cfg);   % Rho = repmat(rho(x0),1,N), Uold = +Inf
+        WS = -ones(B, 2 * (N + 1), 'int32');         % warm-start workspace, carried step to step
         X = X0;
         for k = 1:k_sim
-            [U, ~, Xn, fl, it, Rho, Uold] = ntm_mpc_mex('step', X, Rho, Uold, cfg);
+            [U, ~, Xn, fl, it, Rho, Uold, WS] = ntm_mpc_mex('step', X, Rho, Uold, cfg, WS);
             Uk(:, k, :) = reshape(U.', N, 1, B);
             uk(1, k, :) = reshape(U(:, 1), 1, 1, B);
             exitflag(k, :) = fl.'; iters(k, :) = it.';

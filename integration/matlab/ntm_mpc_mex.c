@@ -11,11 +11,13 @@
  * Calls (every batched array is B-by-E: one row per scenario, which is the
  * ABI's scenario-minor layout [e*B + s] in MATLAB's column-major storage):
  *
- *   [U, x_pred, x_next, exitflag, iters, rho, Uold] = ...
- *       ntm_mpc_mex('step', x_k, rho, Uold, cfg)
+ *   [U, x_pred, x_next, exitflag, iters, rho, Uold, ws] = ...
+ *       ntm_mpc_mex('step', x_k, rho, Uold, cfg[, ws])
  *         x_k  B-by-2        current state [w, omega]           (xk(:,k)')
  *         rho  B-by-3N       reshape(Rho, 1, 3N) per scenario   (:63-65,116)
  *         Uold B-by-N        +Inf on the first step (D14)
+ *         ws   B-by-2(N+1)   optional int32 warm-start workspace (start with
+ *                            -1 everywhere; pass the returned one back next step)
  *   [rho, Uold] = ntm_mpc_mex('init', x0, cfg)                 (:63-65, :86)
  *   [xk, uk, Uk, wpred, exitflag, iters] = ntm_mpc_mex('run', x0, k_sim, cfg)
  *   ntm_mpc_mex('close')
@@ -96,7 +98,7 @@ static const double* in_matrix(const mxArray* a, size_t rows, size_t cols, const
 }
 
 static void do_step(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
-    if (nrhs < 4) mexErrMsgIdAndTxt("ntm:arg", "usage: ntm_mpc_mex('step', x_k, rho, Uold[, cfg])");
+    if (nrhs < 4) mexErrMsgIdAndTxt("ntm:arg", "usage: ntm_mpc_mex('step', x_k, rho, Uold[, cfg[, ws]])");
     const ntm_config c = read_cfg(nrhs > 4 ? prhs[4] : NULL);
     ntm_physics p;
     ntm_physics_default(&p);
@@ -112,11 +114,22 @@ static void do_step(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) 
     mxArray* xn = mxCreateDoubleMatrix(B, 2, mxREAL);
     mxArray* fl = mxCreateNumericMatrix(B, 1, mxINT32_CLASS, mxREAL);
     mxArray* it = mxCreateNumericMatrix(B, 1, mxINT32_CLASS, mxREAL);
-    check(ntm_mpc_step(ctx(), &p, &c, (int64_t)B, x, mxGetDoubles(rho), mxGetDoubles(uold), mxGetDoubles(U),
-                       mxGetDoubles(xp), mxGetDoubles(xn), mxGetInt32s(fl), mxGetInt32s(it)),
-          "ntm_mpc_step");
-    mxArray* outs[7] = {U, xp, xn, fl, it, rho, uold};
-    for (int i = 0; i < 7; ++i) {
+    mxArray* ws = NULL;
+    if (nrhs > 5) {
+        const mxArray* w = prhs[5];
+        if (!mxIsInt32(w) || mxGetM(w) != B || mxGetN(w) != 2 * (N + 1))
+            mexErrMsgIdAndTxt("ntm:arg", "ws must be an int32 %d-by-%d array", (int)B, (int)(2 * (N + 1)));
+        ws = mxDuplicateArray(w);
+    } else {
+        ws = mxCreateNumericMatrix(B, 2 * (N + 1), mxINT32_CLASS, mxREAL);
+        int32_t* wp = mxGetInt32s(ws);
+        for (size_t i = 0; i < B * 2 * (N + 1); ++i) wp[i] = -1;
+    }
+    check(ntm_mpc_step_ws(ctx(), &p, &c, (int64_t)B, x, mxGetDoubles(rho), mxGetDoubles(uold), mxGetDoubles(U),
+                          mxGetDoubles(xp), mxGetDoubles(xn), mxGetInt32s(fl), mxGetInt32s(it), mxGetInt32s(ws)),
+          "ntm_mpc_step_ws");
+    mxArray* outs[8] = {U, xp, xn, fl, it, rho, uold, ws};
+    for (int i = 0; i < 8; ++i) {
         if (i < (nlhs > 0 ? nlhs : 1)) plhs[i] = outs[i];
         else mxDestroyArray(outs[i]);
     }
