@@ -98,7 +98,8 @@ __shared__ unsigned long long ntm_lds_stamps[NTM_NSTAMPS];   // per block (= per
 #endif
 enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL, ST_GI_FACT, ST_GI_CHECK,
        ST_GI_DIR, ST_GI_ADD, ST_GI_DROP, CN_CHECK, CN_CAND, CN_HIT,
-       ST_P_CLASS, ST_P_GRAM, ST_P_CHOL, ST_P_SCHUR, ST_P_BWD, ST_P_KKT, CN_REPAIR, CN_GIRUN };
+       ST_P_CLASS, ST_P_GRAM, ST_P_CHOL, ST_P_SCHUR, ST_P_BWD, ST_P_KKT, CN_REPAIR, CN_GIRUN,
+       ST_S_E, ST_S_Y, ST_S_K, ST_S_CHOL, ST_S_SOLVE };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 constexpr int kMaxNT = 32;         // explicit R^{-1} in GI up to this horizon (WS::useT)
 constexpr int kRepairs = 8;        // single-row repairs of a failed warm-start candidate
@@ -728,7 +729,8 @@ struct StructRows {
     // GI's stopping tolerance: GI may add any violated row, so this only
     // steers it towards the nearby active set.
     template <int P, class W>
-    __device__ __forceinline__ Pick check(const W& w, double Vl, int l, bool verify = false, double vmax = 1.0) const {
+    __device__ __forceinline__ Pick check(const W& w, double Vl, int l, bool verify = false, double vmax = 1.0,
+                                          const double* y_pre = nullptr) const {   // y_pre[r] = Gamma_r U if given
         const int N = w.n();
         if (mode == NTM_MODE_NONE) { Pick none; none.p = verify ? 0 : -1; none.s = 0.0; none.bc = 0.0; return none; }
         double bv = kInf, bs = 0.0, bbc = 0.0;
@@ -762,11 +764,15 @@ struct StructRows {
                     int jmax = r >> 1;
                     const double* gr = w.Gt() + r;           // gt(r, j) = gr[gidx(0, j)]
                     double xh = 0.0;
-                    // fixed trip count (unrolls); entries j > jmax are masked.  The packed
-                    // reads stay inside Gt: gidx(0, j) + r = j(2N-j-1) + r < N(N+1)
-                    for (int j = 0; j < N; ++j) {
-                        const double g = gr[w.gidx(0, j)];
-                        xh += (j <= jmax ? g : 0.0) * w.U()[j];
+                    if (y_pre) {
+                        xh = y_pre[r];
+                    } else {
+                        // fixed trip count (unrolls); entries j > jmax are masked.  The packed
+                        // reads stay inside Gt: gidx(0, j) + r = j(2N-j-1) + r < N(N+1)
+                        for (int j = 0; j < N; ++j) {
+                            const double g = gr[w.gidx(0, j)];
+                            xh += (j <= jmax ? g : 0.0) * w.U()[j];
+                        }
                     }
                     const double er = w.e()[r];
                     xh += er;
@@ -1538,6 +1544,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
                 }
             }
             NTM_WSYNC();
+            NTM_ACC(ST_S_E, tp);
             if (l < nS) {                          // Y = L^{-1} E': lane s solves column s
                 for (int i = 0; i < nF; ++i) {
                     double y = w.J()[i * LDJ + l];
@@ -1546,6 +1553,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
                 }
             }
             NTM_WSYNC();
+            NTM_ACC(ST_S_Y, tp);
             double* K = w.R() + LD;                // K(a, c), a >= c, at R[c + (a+1) LD]
             double rhs = 0.0;
             {
@@ -1565,7 +1573,9 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
                 for (int i = 0; i < nF; ++i) rhs += w.J()[i * LDJ + l] * w.d()[i];
             }
             NTM_WSYNC();
+            NTM_ACC(ST_S_K, tp);
             ok = chol_inplace<P>(K, nS, LD, 1, l, w.kdi());
+            NTM_ACC(ST_S_CHOL, tp);
             if (!ok) fk = 3;
             if (ok) {
                 double t1 = fwd_lanes<P>(K, w.kdi(), nS, LD, 1, rhs, l);
@@ -1577,6 +1587,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
                     for (int a = 0; a < nS; ++a) sY += w.J()[l * LDJ + a] * w.np()[a];
                     tl = sY - wl;
                 }
+                NTM_ACC(ST_S_SOLVE, tp);
             }
         }
         NTM_ACC(ST_P_SCHUR, tp);
@@ -1591,20 +1602,21 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
         // ---- KKT certificate ----
         if (l < N) { w.V()[l] = vfin; w.U()[l] = w.D()[l] * vfin; }
         NTM_WSYNC();
-        double vmax = gmax<P>(l < N ? fabs(vfin) : 0.0);
-        Pick vf = rows.template check<P>(w, vfin, l, true, fmax(1.0, vmax));
-        ok = vf.p == 0;
-        // gradient G~V + F~ = D (2 Gamma' Om (Gamma D V) ) + F~ through Gamma
+        // y = Gamma U once, for the primal check (state rows) and the gradient
         for (int r = l; r < 2 * N; r += P) {
             const int jm = r >> 1;
             double y = 0.0;
             for (int j = 0; j < N; ++j) {
                 const double g = w.gt(r, j);
-                y += (j <= jm) ? g * w.U()[j] : 0.0;
+                y += (j <= jm ? g : 0.0) * w.U()[j];
             }
             w.xp()[r] = y;
         }
         NTM_WSYNC();
+        double vmax = gmax<P>(l < N ? fabs(vfin) : 0.0);
+        Pick vf = rows.template check<P>(w, vfin, l, true, fmax(1.0, vmax), w.xp());
+        ok = vf.p == 0;
+        // gradient G~V + F~ = D (2 Gamma' Om y) + F~
         double res = 0.0;
         if (l < N) {
             const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;
