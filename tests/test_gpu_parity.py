@@ -184,7 +184,7 @@ def test_quadprog_matches_oracle(ctl, mode):
 @pytest.mark.parametrize("N,mode,warm", [(10, 0, False), (20, 1, False), (20, 2, False), (3, 2, False),
                                          (50, 2, False), (50, 1, False), (20, 2, True), (20, 1, True),
                                          (50, 2, True), (20, 3, False), (20, 3, True), (4, 3, False),
-                                         (50, 3, True)])
+                                         (50, 3, True), (1, 2, False), (1, 1, True), (64, 2, True)])
 def test_step_teacher_forced(ctl, N, mode, warm):
     """Each step, the GPU and the oracle get identical (x_k, rho, U_old); with
     warm=True the GPU also carries its active-set workspace from step to step
@@ -197,7 +197,7 @@ def test_step_teacher_forced(ctl, N, mode, warm):
     sets, and a scenario whose path diverged (different inner-iteration count,
     DESIGN.md §3) legitimately ends elsewhere: there only the scenarios that
     took the same path are compared, and >= 90% of them must."""
-    B, k_sim = 48, 12 if N < 50 else 4
+    B, k_sim = (48, 12) if N < 50 else ((48, 4) if N == 50 else (16, 3))
     cfg, ocfg = cfgs(N, mode)
     x = O.scenario_x0(np.arange(B)).T if mode else np.tile(O.REFERENCE_X0[:, None], (1, B))
     rho, Uo = cbind.initial_state(x, ocfg)
@@ -377,3 +377,21 @@ def test_step_workspace_roundtrip_host(ctl):
         np.testing.assert_array_equal(wh, H(ws))
         x0 = np.ascontiguousarray(hs["x_next"])
     assert (wh[N] >= 0).all()                                          # slots hold active sets
+
+
+def test_empty_batch_and_invalid_arguments(ctl):
+    """B = 0 is a no-op; out-of-range N, an unknown mode or a non-finite du_max
+    are API errors (NTM_E_INVALID with a message), not solver outcomes."""
+    from ntm_mpc import NtmLibraryError
+    N = 20
+    cfg, _ = cfgs(N, 2)
+    x = torch.empty(2, 0, dtype=torch.float64, device=DEV)
+    rho, uo = ctl.initial_state(x, cfg)
+    out = ctl.step(x, rho, uo, cfg)
+    assert out["U"].shape == (N, 0) and out["exitflag"].shape == (0,)
+    x1 = T(O.scenario_x0(np.arange(2)).T)
+    for bad in (dict(N=0), dict(N=65), dict(mode=4), dict(mode=3, du_max=float("nan"))):
+        c = cfgs(bad.pop("N", N), bad.pop("mode", 2), **bad)[0]
+        with pytest.raises(NtmLibraryError):
+            r, u = ctl.initial_state(x1, c)
+            ctl.step(x1, r, u, c)
