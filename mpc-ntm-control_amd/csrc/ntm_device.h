@@ -99,7 +99,7 @@ __shared__ unsigned long long ntm_lds_stamps[NTM_NSTAMPS];   // per block (= per
 enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL, ST_GI_FACT, ST_GI_CHECK,
        ST_GI_DIR, ST_GI_ADD, ST_GI_DROP, CN_CHECK, CN_CAND, CN_HIT,
        ST_P_CLASS, ST_P_GRAM, ST_P_CHOL, ST_P_SCHUR, ST_P_BWD, ST_P_KKT, CN_REPAIR, CN_GIRUN,
-       ST_S_E, ST_S_Y, ST_S_K, ST_S_CHOL, ST_S_SOLVE };
+       ST_S_E, ST_S_Y, ST_S_K, ST_S_CHOL, ST_S_SOLVE, CN_TRY_EARLY, CN_FAIL_EARLY, CN_FAIL_LATE };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 constexpr int kMaxNT = 32;         // explicit R^{-1} in GI up to this horizon (WS::useT)
 constexpr int kRepairs = 8;        // single-row repairs of a failed warm-start candidate
@@ -1721,7 +1721,8 @@ __device__ __forceinline__ void plant_step(const Prob& pb, double x0, double x1,
 // ---------------------------------------------------------------------------
 template <int P, class W>
 __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l, int* qp_iters,
-                        int* q_out, int* ns_out, int slot, int* n_try = nullptr, int* n_girun = nullptr) {
+                        int* q_out, int* ns_out, int slot, int* n_try = nullptr, int* n_girun = nullptr,
+                        int it = 0) {
     const int N = w.n();
     NTM_T0(tq);
     lift_phase<P>(pb, w, l);
@@ -1767,6 +1768,10 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                     double vf = 0.0;
                     const bool okc = polish_compact<P>(pb, w, rows, cq, l, true, &ns, &fk, &fp, &vf);
                     NTM_TRACE("QP cand rep %d cq %d ok %d fk %d fp %d\n", rep, cq, (int)okc, fk, fp);
+                    if (rep == 0) {
+                        if (it <= 2) NTM_CNT(CN_TRY_EARLY);
+                        if (!okc) { if (it <= 2) NTM_CNT(CN_FAIL_EARLY); else NTM_CNT(CN_FAIL_LATE); }
+                    }
                     if (okc) {
                         flag = NTM_EXIT_OPTIMAL;
                         q = cq;

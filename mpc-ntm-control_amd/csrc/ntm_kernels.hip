@@ -89,7 +89,7 @@ __device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x
     int n_qp = 0, n_gi = 0, n_act = 0, n_gen = 0, n_try = 0, n_girun = 0;
     for (it = 1; it <= pb.i_sim; ++it) {
         int qi = 0, qa = 0, ns = 0;
-        flag = qp_phase<P>(pb, w, x0, x1, l, &qi, &qa, &ns, (it - 1) & 1, &n_try, &n_girun);
+        flag = qp_phase<P>(pb, w, x0, x1, l, &qi, &qa, &ns, (it - 1) & 1, &n_try, &n_girun, it);
         ++n_qp;
         n_gi += qi;
         n_act += qa;

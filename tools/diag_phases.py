@@ -30,6 +30,7 @@ sub = "p_class p_gram p_chol p_schur p_bwd p_kkt".split()
 print("certified re-solve (cand + polish) sub-phases, cycles per wave-step:")
 for i, n in enumerate(sub):
     print(f"  {n:9s} {buf[16 + i]/B:12.0f}")
+print(f"  first tries at it<=2: {buf[29]/B:.2f}, failed {buf[30]/B:.2f}; failed at it>2: {buf[31]/B:.2f}")
 sch = "s_E+h s_Y s_K s_cholK s_solve".split()
 print("  Schur part:")
 for i, n in enumerate(sch):
