@@ -49,6 +49,17 @@ struct Prob {
 
 constexpr double kInf = __builtin_huge_val();
 
+// 1/sqrt(x) for x > 0: v_rsq_f64 plus two Newton steps (full fp64 accuracy;
+// the pivots of the small Cholesky factorisations sit on their sequential
+// critical path, where the IEEE sqrt + division expansions cost ~25 dependent ops)
+__device__ __forceinline__ double rsqrt_nr(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    const double h = 0.5 * x;
+    y = fma(y, fma(-h * y, y, 0.5), y);
+    y = fma(y, fma(-h * y, y, 0.5), y);
+    return y;
+}
+
 // Trace build only (make trace NTM_DEBUG_SCEN=s): printf GI's iterations for
 // one scenario.  The production library compiles every trace away.
 #ifdef NTM_DEBUG_SCEN
@@ -508,20 +519,25 @@ __device__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_st
     const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
     int bad = 0;
     if (l < N) {
+        // one pass over Gamma's column l: the Gram diagonal G_ll and F_l = 2 Gamma_l' Om (e - r)
         const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
-        double s = 0.0;
+        const double r0 = pb.r[0], r1 = pb.r[1];
+        double s = 0.0, fs = 0.0;
         for (int i = 0; i < N; ++i) {            // fixed trip count, terms i < l masked
             const double g0 = cj[2 * i], g1 = cj[2 * i + 1];
             const double o0 = q00 * g0 + q01 * g1;
             const double o1 = q10 * g0 + q11 * g1;
             const double t = g0 * o0 + g1 * o1;
+            const double e0 = w.e()[2 * i] - r0, e1 = w.e()[2 * i + 1] - r1;
+            const double tf = g0 * (q00 * e0 + q01 * e1) + g1 * (q10 * e0 + q11 * e1);
             if (i >= l) bad |= !isfinite(g0) || !isfinite(g1);
             s += (i >= l) ? t : 0.0;
+            fs += (i >= l) ? tf : 0.0;
         }
         double g = 2 * s;
-        double Dl = (g > 0.0) ? 1.0 / sqrt(g) : 1.0;
+        double Dl = (g > 0.0 && g < kInf) ? rsqrt_nr(g) : 1.0;
         w.D()[l] = Dl;
-        double f = w.F()[l] * Dl;
+        double f = (2 * fs) * Dl;
         bad |= !isfinite(f) || !isfinite(Dl);
         w.F()[l] = f;
         // V-space box of u_l (bc of the two u rows; same expressions as the oracle's b/rn)
@@ -542,9 +558,9 @@ __device__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_st
                 s += (j <= jmax) ? v * v : 0.0;
             }
             bad |= !isfinite(s) || !isfinite(w.e()[r]);
-            double rn = s > 0.0 ? sqrt(s) : 0.0;
-            w.rn()[r] = rn;
-            w.irn()[r] = rn > 0.0 ? 1.0 / rn : 0.0;
+            const double ir = (s > 0.0 && s < kInf) ? rsqrt_nr(s) : 0.0;
+            w.rn()[r] = s * ir;                  // |Gamma_r D|
+            w.irn()[r] = ir;
         }
         NTM_WSYNC();
     }
@@ -882,17 +898,6 @@ struct DenseRows {
 // ---------------------------------------------------------------------------
 // Element (i, j) of a small matrix lives at A[i*RS + j*CS] (col-major: RS = 1,
 // CS = LD; the polish's K is stored transposed: RS = LD, CS = 1).
-// 1/sqrt(x) for x > 0: v_rsq_f64 plus two Newton steps (full fp64 accuracy;
-// the pivots of the small Cholesky factorisations sit on their sequential
-// critical path, where the IEEE sqrt + division expansions cost ~25 dependent ops)
-__device__ __forceinline__ double rsqrt_nr(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-    const double h = 0.5 * x;
-    y = fma(y, fma(-h * y, y, 0.5), y);
-    y = fma(y, fma(-h * y, y, 0.5), y);
-    return y;
-}
-
 // left-looking Cholesky of the n x n lower triangle of A, in place; the
 // reciprocals of the diagonal go to rdiag[0..n) (the triangular solves then
 // multiply instead of divide); false if not PD
@@ -1727,8 +1732,7 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
     NTM_T0(tq);
     lift_phase<P>(pb, w, l);
     NTM_ACC(ST_LIFT, tq);
-    free_response<P>(w, x0, x1, l);
-    f_phase<P>(pb, w, l);
+    free_response<P>(w, x0, x1, l);          // F is formed with the Jacobi scaling below
     NTM_ACC(ST_COST, tq);
     const bool full = pb.mode >= NTM_MODE_FULL;        // state rows present
     int flag, q = 0, ns = 0;
