@@ -597,26 +597,6 @@ __device__ bool scale_phase(const W& w, int l, bool /*with_state_rows*/) {
     return gmaxi<P>(bad) == 0;
 }
 
-// F = 2 Gamma' Om (e - R) only (NTM_MPC_Sim.m:121); G is formed on demand
-template <int P, class W>
-__device__ void f_phase(const Prob& pb, const W& w, int l) {
-    const int N = w.n();
-    const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
-    if (l < N) {
-        const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
-        double f = 0.0;
-        for (int i = 0; i < N; ++i) {            // fixed trip count, terms i < l masked
-            const double e0 = w.e()[2 * i] - pb.r[0], e1 = w.e()[2 * i + 1] - pb.r[1];
-            const double o0 = q00 * e0 + q01 * e1;
-            const double o1 = q10 * e0 + q11 * e1;
-            const double t = cj[2 * i] * o0 + cj[2 * i + 1] * o1;
-            f += (i >= l) ? t : 0.0;
-        }
-        w.F()[l] = 2 * f;
-    }
-    NTM_WSYNC();
-}
-
 // ---------------------------------------------------------------------------
 // Constraint-row providers (Lin U <= b form, getWLc.m row convention).  Row
 // ids follow the oracle: box mode rows 0..N-1 are u_j >= umin, N..2N-1 are

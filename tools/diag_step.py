@@ -1,6 +1,8 @@
 """Diagnostic: find teacher-forced steps where GPU and C oracle disagree; dump inputs."""
 import sys, numpy as np, torch
-sys.path.insert(0,'/root/repo'); sys.path.insert(0,'/root/repo/mpc-ntm-control_amd')
+import os
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), '..')
+sys.path[:0] = [ROOT, os.path.join(ROOT, 'mpc-ntm-control_amd')]
 from ntm_mpc import NtmMpc, Config
 from oracle import ntm_oracle as O, cbind
 ctl=NtmMpc()
