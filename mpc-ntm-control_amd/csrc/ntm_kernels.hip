@@ -114,8 +114,12 @@ __device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x
 #ifndef NTM_HOT_WAVES_PER_EU
 #define NTM_HOT_WAVES_PER_EU 2
 #endif
+// Long horizons (NN > 32): the LDS workspace already limits a CU to fewer waves
+// than SIMDs, so the register budget of one wave per SIMD costs no occupancy and
+// removes the spills of the fully unrolled horizon loops.
+#define NTM_WAVES_PER_EU(NN) ((NN) > 32 ? 1 : NTM_HOT_WAVES_PER_EU)
 template <int P, int NN>
-__global__ __launch_bounds__(64, NTM_HOT_WAVES_PER_EU) void k_mpc_step(Prob pb, int64_t B, const double* __restrict__ x_k,
+__global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, int64_t B, const double* __restrict__ x_k,
                                                  double* __restrict__ rho, double* __restrict__ U_old,
                                                  double* __restrict__ U, double* __restrict__ x_pred,
                                                  double* __restrict__ x_next, int32_t* __restrict__ exitflag,
@@ -155,7 +159,7 @@ __global__ __launch_bounds__(64, NTM_HOT_WAVES_PER_EU) void k_mpc_step(Prob pb, 
 }
 
 template <int P, int NN>
-__global__ __launch_bounds__(64, NTM_HOT_WAVES_PER_EU) void k_mpc_run(Prob pb, int64_t B, int k_sim, const double* __restrict__ x0v,
+__global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_run(Prob pb, int64_t B, int k_sim, const double* __restrict__ x0v,
                                                 double* xk, double* uk, double* Uk, double* wpred,
                                                 int32_t* exitflag, int32_t* inner_iters) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
