@@ -51,30 +51,57 @@ def parse():
     return ap.parse_args()
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(N, mode, target_s):
     """C restatement of the oracle (oracle/ntm_oracle.c, the "port"), OpenMP over
-    scenarios on this host, timed on a bounded sample of the same workload."""
+    scenarios on this host, timed on a bounded sample of the same workload; plus
+    the same on one core and the NumPy oracle (single thread, the interpreted
+    stand-in for MATLAB) on a few scenarios (BASELINE.md CPU-baseline plan)."""
     import numpy as np
     from oracle import cbind
     from oracle import ntm_oracle as O
+    import ntm_mpc
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
     threads = max(1, min(threads, os.cpu_count() or 1))
     cfg = O.Config(N=N, mode=mode)
-    import ntm_mpc
     k = 2
+
+    def timed(B, nthreads):
+        x0 = ntm_mpc.scenarios_x0(0, B)
+        t = time.perf_counter()
+        cbind.run(x0, cfg, k, nthreads=nthreads)
+        return time.perf_counter() - t
+
     B = 64 * threads
-    x0 = ntm_mpc.scenarios_x0(0, B)
-    t = time.perf_counter()
-    cbind.run(x0, cfg, k, nthreads=threads)
-    dt = time.perf_counter() - t
+    dt = timed(B, threads)
     B2 = int(min(400_000, max(B, B * target_s / max(dt, 1e-3))))
-    x0 = ntm_mpc.scenarios_x0(0, B2)
+    dt = timed(B2, threads)
+    b1 = 64
+    d1 = timed(b1, 1)
+    b1 = int(min(20_000, max(b1, b1 * 3.0 / max(d1, 1e-3))))   # ~3 s on one core
+    d1 = timed(b1, 1)
+    ph, nb = O.Physics(), 30
     t = time.perf_counter()
-    cbind.run(x0, cfg, k, nthreads=threads)
-    dt = time.perf_counter() - t
+    for s in range(nb):                                         # NumPy oracle, one step each
+        x = ntm_mpc.scenarios_x0(s, 1)[:, 0]
+        O.mpc_step(x, O.initial_rho(x, ph, cfg), np.full(N, np.inf), ph, cfg)
+    dpy = time.perf_counter() - t
     return {"value": B2 * k / dt, "unit": "MPC steps/s", "cores": threads, "kind": "port",
             "sample": f"{B2} scenarios x {k} closed-loop steps (ids 0..{B2 - 1}), N={N}, mode={mode}, "
-                      f"{threads} OpenMP threads, {dt:.1f} s"}
+                      f"{threads} OpenMP threads, {dt:.1f} s",
+            "one_core_value": b1 * k / d1, "one_core_sample": f"{b1} scenarios x {k} steps, 1 thread, {d1:.1f} s",
+            "interpreted_numpy_value": nb / dpy,
+            "interpreted_sample": f"NumPy oracle, {nb} scenarios x 1 step, 1 thread, {dpy:.1f} s",
+            "host": {"nproc": os.cpu_count(), "cpu_model": _cpu_model()}}
 
 
 def main():
