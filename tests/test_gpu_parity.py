@@ -395,3 +395,45 @@ def test_empty_batch_and_invalid_arguments(ctl):
         with pytest.raises(NtmLibraryError):
             r, u = ctl.initial_state(x1, c)
             ctl.step(x1, r, u, c)
+
+
+@pytest.mark.parametrize("N,mode", [(20, 2), (50, 3)])
+def test_full_size_batch_properties(ctl, N, mode):
+    """BASELINE configs 3 (N = 20, full getWLc rows) and 5 (N = 50, + rate rows)
+    at full size (B = 1e5), one step with the carried workspace, checked by
+    size-independent properties:
+      * every scenario is solved (exitflag 1) and its plan is feasible: U within
+        [umin, umax] and the predicted states x^_1..x^_N within [xmin, xmax]
+        (the getWLc rows), to 1e-9 relative;
+      * a seeded sample of 64 scenarios matches the oracle (teacher-forced);
+      * batch-composition invariance: the same 64 scenarios run as their own
+        batch give bit-identical outputs (no cross-scenario coupling)."""
+    import ntm_mpc
+    B = 100_000
+    cfg, ocfg = cfgs(N, mode)
+    x = torch.tensor(ntm_mpc.scenarios_x0(0, B), device=DEV)
+    rho, uo = ctl.initial_state(x, cfg)
+    ws = ctl.new_active_ws(B, cfg)
+    out = ctl.step(x, rho, uo, cfg, active_ws=ws)             # step 1 fills the workspace
+    x2, rho2, uo2, ws2 = out["x_next"].clone(), rho.clone(), uo.clone(), ws.clone()
+    rho_in, uo_in = rho2.clone(), uo2.clone()
+    out = ctl.step(x2, rho2, uo2, cfg, active_ws=ws2)        # the measured step
+    flags = H(out["exitflag"])
+    assert (flags == 1).all()
+    U = H(out["U"])
+    assert U.min() >= cfg.umin - 1e-9 * cfg.umax and U.max() <= cfg.umax * (1 + 1e-9)
+    xp = H(out["x_pred"]).reshape(N + 1, 2, B)[1:]            # x^_1..x^_N
+    for c in range(2):
+        span = cfg.xmax[c] - cfg.xmin[c]
+        assert xp[:, c].min() >= cfg.xmin[c] - 1e-9 * span and xp[:, c].max() <= cfg.xmax[c] + 1e-9 * span
+    if mode == 3:                                             # rate rows |U_i - U_{i-1}| <= du_max
+        assert np.max(np.abs(np.diff(U, axis=0))) <= cfg.du_max * (1 + 1e-9)
+    ids = np.sort(np.random.default_rng(5).choice(B, 64, replace=False))
+    xs, rs, us = H(x2)[:, ids], H(rho_in)[:, ids], H(uo_in)[:, ids]
+    ref = cbind.step(np.ascontiguousarray(xs), np.ascontiguousarray(rs), np.ascontiguousarray(us), ocfg)
+    same = H(out["inner_iters"])[ids] == ref["inner_iters"]
+    assert same.mean() >= 0.9
+    assert np.max(np.abs(U[:, ids] - ref["U"])[:, same]) / cfg.umax <= (U_TOL_RATE if mode == 3 else U_TOL)
+    sub = ctl.step(T(xs), T(rs), T(us), cfg, active_ws=ws[:, ids].contiguous())
+    for k in ("U", "x_pred", "x_next", "exitflag", "inner_iters"):
+        np.testing.assert_array_equal(H(sub[k]), H(out[k])[..., ids], err_msg=k)
