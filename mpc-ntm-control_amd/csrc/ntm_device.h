@@ -1428,7 +1428,10 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
     const bool fixed = (l < N) && w.fx()[l];
     const double uf = fixed ? w.Uf()[l] : 0.0;
     const double vb = fixed ? uf / w.D()[l] : 0.0;
-    if (l < N) w.Vb()[l] = vb;
+    if (l < N) {
+        w.Vb()[l] = vb;
+        w.dr()[l] = uf;                                   // U_B: fixed values, 0 on free variables
+    }
     // --- compact map of the free variables ---
     bal = __ballot((l < N) && !fixed) & gmask;
     const int nF = uni<P>((int)__popcll(bal));
@@ -1436,12 +1439,13 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
     if (l < N && !fixed) w.fidx()[fpos] = l;
     // --- y_B = Gamma U_B (fixed variables only; scratch in w.Phi(), dead until the
     //     next lift) and z = y_B + e - r (scratch in w.xp(), rewritten by the rollout) ---
+    NTM_WSYNC();
     for (int r = l; r < 2 * N; r += P) {
         const int jm = r >> 1;
         double y = 0.0;
         for (int j = 0; j < N; ++j) {
             const double g = w.gt(r, j);
-            y += (j <= jm && w.fx()[j]) ? g * w.Uf()[j] : 0.0;
+            y += (j <= jm ? g : 0.0) * w.dr()[j];
         }
         w.Phi()[r] = y;
         w.xp()[r] = y + w.e()[r] - ((r & 1) ? pb.r[1] : pb.r[0]);
