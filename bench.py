@@ -231,7 +231,7 @@ def main():
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": ctl.step_kernel_name(B, cfg), "kernel_avg_ms": kern_ms,
                      "flop_per_step": flop_step,
-                     "hbm_algorithmic_bytes_per_launch": FL.hbm_bytes_per_step(N) * B,
+                     "hbm_algorithmic_bytes_per_launch": FL.hbm_bytes_per_step(N, workspace=True) * B,
                      "note": "fp64 VALU work; peak = MI355X dense fp64 (vector == matrix rate)"},
         "solver": {"inner_iters_mean": iters, "qp_per_step": qps, "warm_verify_per_step": tries,
                    "gi_solves_per_step": giruns, "gi_iters_per_step": Kgi,

@@ -91,8 +91,10 @@ def per_step(N: int, mode: int, qps: float, tries: float, giruns: float, K: floa
     return f + 30.0                                   # plant step
 
 
-def hbm_bytes_per_step(N: int) -> int:
+def hbm_bytes_per_step(N: int, workspace: bool = False) -> int:
     """Algorithmic HBM bytes of one MPC step (state in/out + outputs), SURVEY §8(d):
     x_k (2), rho in/out (2*3N), U_old in/out (2N), U (N), x_pred (2(N+1)),
-    x_next (2) doubles + exitflag, inner_iters (int32)."""
-    return 8 * (2 + 6 * N + 2 * N + N + 2 * (N + 1) + 2) + 8
+    x_next (2) doubles + exitflag, inner_iters (int32); with ``workspace`` also
+    the warm-start active sets in and out (2 x 2(N+1) int32, ntm_mpc_step_ws)."""
+    ws = 2 * 4 * 2 * (N + 1) if workspace else 0
+    return 8 * (2 + 6 * N + 2 * N + N + 2 * (N + 1) + 2) + 8 + ws

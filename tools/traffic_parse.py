@@ -42,7 +42,8 @@ res = {
     "write_bytes_per_launch": w_step,
     # the guide's prescribed correction: FETCH_SIZE x2 (it tallies 128-B requests at 64 B)
     "hbm_bytes_per_launch": 2 * f_step + w_step,
-    "algorithmic_bytes_per_launch": B * (8 * (2 + 6 * 20 + 2 * 20 + 20 + 2 * 21 + 2) + 8),
+    # state in/out + outputs (1816 B) + warm-start workspace in/out (336 B), as flops.hbm_bytes_per_step
+    "algorithmic_bytes_per_launch": B * (8 * (2 + 6 * 20 + 2 * 20 + 20 + 2 * 21 + 2) + 8 + 2 * 4 * 2 * 21),
     "calibration": {"copy_bytes_each_way": cal_bytes,
                     "fetch_reported": None if f_cal is None else f_cal * KB,
                     "write_reported": None if w_cal is None else w_cal * KB},
