@@ -133,7 +133,7 @@ def main():
     ctl = NtmMpc(config=cfg, device=local)
     dev = f"cuda:{local}"
     # shard: global scenario ids [rank*B, (rank+1)*B)  (shard-invariant inputs)
-    x = torch.tensor(ntm_mpc.scenarios_x0(rank * B, B), device=dev)
+    x = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(rank * B, B), local)
     rho, U_old = ctl.initial_state(x, cfg)
     active_ws = ctl.new_active_ws(B, cfg)       # last two active sets, carried step to step
     outs = [None, None]

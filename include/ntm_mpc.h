@@ -12,8 +12,13 @@
  *
  * Conventions
  *  - fp64 everywhere; all per-scenario matrices are MATLAB column-major.
- *  - Batched arrays are scenario-minor ("SoA"): element e of scenario s lives
- *    at [e*B + s].  In MATLAB this is simply a B-by-E array.
+ *  - Batched arrays are scenario-major: a per-scenario record of E elements
+ *    is contiguous, element e of scenario s at [s*E + e].  In MATLAB this is
+ *    an E-by-B array with one column per scenario (x0 is 2-by-B, U is N-by-B,
+ *    rho is 3N-by-B), and a contiguous range of scenarios (one GPU's shard) is
+ *    a contiguous block of memory.  The time histories of ntm_mpc_run are
+ *    E-by-k_sim-by-B.  (ABI v2 was scenario-minor, [e*B + s].)
+ *    Exception: the optional instrumentation counters (ntm_ctx_set_stats).
  *  - Host-pointer entry points (no suffix) stage through the device and are
  *    synchronous.  *_device entry points take device pointers and a
  *    hipStream_t (as void*), enqueue only, and never synchronise.
@@ -32,7 +37,7 @@
 extern "C" {
 #endif
 
-#define NTM_MPC_ABI_VERSION 2
+#define NTM_MPC_ABI_VERSION 3
 #define NTM_MAX_N 64
 
 /* Physics constants, NTM_MPC_Sim.m:5-22 (same names and units). */
@@ -147,9 +152,10 @@ int ntm_mpc_step_ws_device(ntm_ctx* ctx, const ntm_physics* phys,
                            int32_t* active_ws, void* stream);
 
 /* Closed loop NTM_MPC_Sim.m:80-131 over k_sim steps, device-resident.
- * x0[2]; outputs xk[2(k_sim+1)] (2x(k_sim+1)), uk[k_sim], Uk[N k_sim]
- * (N x k_sim), wpred[(N+1) k_sim] (predicted island width per step),
- * exitflag[k_sim], inner_iters[k_sim].  Any output pointer may be NULL. */
+ * Per scenario: x0[2]; outputs xk[2(k_sim+1)] (2x(k_sim+1)), uk[k_sim],
+ * Uk[N k_sim] (N x k_sim), wpred[(N+1) k_sim] ((N+1) x k_sim, predicted island
+ * width per step), exitflag[k_sim], inner_iters[k_sim].  Any output pointer
+ * may be NULL. */
 int ntm_mpc_run(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg,
                 int64_t B, int32_t k_sim, const double* x0, double* xk,
                 double* uk, double* Uk, double* wpred, int32_t* exitflag,
@@ -188,7 +194,7 @@ int ntm_qp_device(ntm_ctx* ctx, int64_t B, int32_t N, int32_t m,
                   int32_t* iters, void* stream);
 
 /* Synthetic scenarios, counter-based and shard-invariant:
- * x0 for global scenario ids first_id .. first_id+B-1 (host array 2xB SoA). */
+ * x0 for global scenario ids first_id .. first_id+B-1 (host array, 2 per scenario). */
 void ntm_scenarios_x0(uint64_t seed, int64_t first_id, int64_t B, double* x0);
 
 #ifdef __cplusplus

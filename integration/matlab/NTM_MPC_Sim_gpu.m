@@ -15,6 +15,9 @@ function [xk, uk, Uk, exitflag, iters] = NTM_MPC_Sim_gpu(x0, k_sim, cfg, mode)
 %   dimension: xk 2-by-(k_sim+1)-by-B, uk 1-by-k_sim-by-B, Uk N-by-k_sim-by-B,
 %   plus exitflag / iters (k_sim-by-B, quadprog codes and LPV iterations).
 %
+%   The MEX takes and returns E-by-B arrays (one column per scenario, the
+%   ABI's scenario-major layout), so nothing is transposed on the way.
+%
 %   Semantics are the repaired ones of SURVEY.md §2.1 (CANON): Phi_i = A_i
 %   Phi_{i-1}, Gamma_ij = A_i Gamma_{i-1,j}, W/L/c rebuilt each iteration, F
 %   from the current x_k, plant step with +C, Uold = +Inf at start.
@@ -23,29 +26,28 @@ if nargin < 4, mode = 'run'; end
 if ~isfield(cfg, 'N'), cfg.N = 20; end
 N = cfg.N;
 B = size(x0, 2);
-X0 = x0.';                                   % B-by-2: the ABI's scenario-minor layout
 switch mode
     case 'run'
-        [XK, UK, UKK, ~, FL, IT] = ntm_mpc_mex('run', X0, k_sim, cfg);
-        xk = permute(reshape(XK, B, 2, k_sim + 1), [2 3 1]);
-        uk = permute(reshape(UK, B, 1, k_sim), [2 3 1]);
-        Uk = permute(reshape(UKK, B, N, k_sim), [2 3 1]);
-        exitflag = FL.';
-        iters = IT.';
+        [XK, UK, UKK, ~, FL, IT] = ntm_mpc_mex('run', x0, k_sim, cfg);
+        xk = reshape(XK, 2, k_sim + 1, B);
+        uk = reshape(UK, 1, k_sim, B);
+        Uk = reshape(UKK, N, k_sim, B);
+        exitflag = FL;
+        iters = IT;
     case 'step'
         xk = zeros(2, k_sim + 1, B); uk = zeros(1, k_sim, B); Uk = zeros(N, k_sim, B);
         exitflag = zeros(k_sim, B, 'int32'); iters = zeros(k_sim, B, 'int32');
         xk(:, 1, :) = reshape(x0, 2, 1, B);
-        [Rho, Uold] = ntm_mpc_mex('init', X0, cfg);   % Rho = repmat(rho(x0),1,N), Uold = +Inf
-        WS = -ones(B, 2 * (N + 1), 'int32');         % warm-start workspace, carried step to step
-        X = X0;
+        [Rho, Uold] = ntm_mpc_mex('init', x0, cfg);   % Rho = repmat(rho(x0),1,N), Uold = +Inf
+        WS = -ones(2 * (N + 1), B, 'int32');         % warm-start workspace, carried step to step
+        X = x0;
         for k = 1:k_sim
             [U, ~, Xn, fl, it, Rho, Uold, WS] = ntm_mpc_mex('step', X, Rho, Uold, cfg, WS);
-            Uk(:, k, :) = reshape(U.', N, 1, B);
-            uk(1, k, :) = reshape(U(:, 1), 1, 1, B);
-            exitflag(k, :) = fl.'; iters(k, :) = it.';
+            Uk(:, k, :) = reshape(U, N, 1, B);
+            uk(1, k, :) = reshape(U(1, :), 1, 1, B);
+            exitflag(k, :) = fl; iters(k, :) = it;
             X = Xn;
-            xk(:, k + 1, :) = reshape(Xn.', 2, 1, B);
+            xk(:, k + 1, :) = reshape(Xn, 2, 1, B);
         end
     otherwise
         error('ntm:arg', 'mode must be ''run'' or ''step''');

@@ -8,18 +8,23 @@
  *   mex -R2018a -I../../include ntm_mpc_mex.c \
  *       -L../../mpc-ntm-control_amd/lib -lntm_mpc
  *
- * Calls (every batched array is B-by-E: one row per scenario, which is the
- * ABI's scenario-minor layout [e*B + s] in MATLAB's column-major storage):
+ * Calls (every batched array is E-by-B: one column per scenario, which is the
+ * ABI's scenario-major layout [s*E + e] in MATLAB's column-major storage, so
+ * arrays pass through without copies):
  *
  *   [U, x_pred, x_next, exitflag, iters, rho, Uold, ws] = ...
  *       ntm_mpc_mex('step', x_k, rho, Uold, cfg[, ws])
- *         x_k  B-by-2        current state [w, omega]           (xk(:,k)')
- *         rho  B-by-3N       reshape(Rho, 1, 3N) per scenario   (:63-65,116)
- *         Uold B-by-N        +Inf on the first step (D14)
- *         ws   B-by-2(N+1)   optional int32 warm-start workspace (start with
+ *         x_k  2-by-B        current state [w; omega]           (xk(:,k))
+ *         rho  3N-by-B       Rho(:) per scenario                (:63-65,116)
+ *         Uold N-by-B        +Inf on the first step (D14)
+ *         ws   2(N+1)-by-B   optional int32 warm-start workspace (start with
  *                            -1 everywhere; pass the returned one back next step)
+ *       outputs: U N-by-B, x_pred 2(N+1)-by-B, x_next 2-by-B, exitflag and
+ *       iters 1-by-B
  *   [rho, Uold] = ntm_mpc_mex('init', x0, cfg)                 (:63-65, :86)
  *   [xk, uk, Uk, wpred, exitflag, iters] = ntm_mpc_mex('run', x0, k_sim, cfg)
+ *       outputs 2(k_sim+1)-by-B, k_sim-by-B, N k_sim-by-B, (N+1) k_sim-by-B,
+ *       k_sim-by-B, k_sim-by-B (per scenario column: xk(:), uk, Uk(:), ...)
  *   ntm_mpc_mex('close')
  *
  * cfg is an optional struct with any of the fields N, i_sim, mode, flags, Ts,
@@ -102,26 +107,26 @@ static void do_step(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) 
     const ntm_config c = read_cfg(nrhs > 4 ? prhs[4] : NULL);
     ntm_physics p;
     ntm_physics_default(&p);
-    const size_t B = mxGetM(prhs[1]), N = (size_t)c.N;
-    const double* x = in_matrix(prhs[1], B, 2, "x_k");
-    in_matrix(prhs[2], B, 3 * N, "rho");
-    in_matrix(prhs[3], B, N, "Uold");
+    const size_t B = mxGetN(prhs[1]), N = (size_t)c.N;
+    const double* x = in_matrix(prhs[1], 2, B, "x_k");
+    in_matrix(prhs[2], 3 * N, B, "rho");
+    in_matrix(prhs[3], N, B, "Uold");
     /* value semantics: rho / Uold are updated in copies returned as outputs 6-7 */
     mxArray* rho = mxDuplicateArray(prhs[2]);
     mxArray* uold = mxDuplicateArray(prhs[3]);
-    mxArray* U = mxCreateDoubleMatrix(B, N, mxREAL);
-    mxArray* xp = mxCreateDoubleMatrix(B, 2 * (N + 1), mxREAL);
-    mxArray* xn = mxCreateDoubleMatrix(B, 2, mxREAL);
-    mxArray* fl = mxCreateNumericMatrix(B, 1, mxINT32_CLASS, mxREAL);
-    mxArray* it = mxCreateNumericMatrix(B, 1, mxINT32_CLASS, mxREAL);
+    mxArray* U = mxCreateDoubleMatrix(N, B, mxREAL);
+    mxArray* xp = mxCreateDoubleMatrix(2 * (N + 1), B, mxREAL);
+    mxArray* xn = mxCreateDoubleMatrix(2, B, mxREAL);
+    mxArray* fl = mxCreateNumericMatrix(1, B, mxINT32_CLASS, mxREAL);
+    mxArray* it = mxCreateNumericMatrix(1, B, mxINT32_CLASS, mxREAL);
     mxArray* ws = NULL;
     if (nrhs > 5) {
         const mxArray* w = prhs[5];
-        if (!mxIsInt32(w) || mxGetM(w) != B || mxGetN(w) != 2 * (N + 1))
-            mexErrMsgIdAndTxt("ntm:arg", "ws must be an int32 %d-by-%d array", (int)B, (int)(2 * (N + 1)));
+        if (!mxIsInt32(w) || mxGetM(w) != 2 * (N + 1) || mxGetN(w) != B)
+            mexErrMsgIdAndTxt("ntm:arg", "ws must be an int32 %d-by-%d array", (int)(2 * (N + 1)), (int)B);
         ws = mxDuplicateArray(w);
     } else {
-        ws = mxCreateNumericMatrix(B, 2 * (N + 1), mxINT32_CLASS, mxREAL);
+        ws = mxCreateNumericMatrix(2 * (N + 1), B, mxINT32_CLASS, mxREAL);
         int32_t* wp = mxGetInt32s(ws);
         for (size_t i = 0; i < B * 2 * (N + 1); ++i) wp[i] = -1;
     }
@@ -140,10 +145,10 @@ static void do_init(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) 
     const ntm_config c = read_cfg(nrhs > 2 ? prhs[2] : NULL);
     ntm_physics p;
     ntm_physics_default(&p);
-    const size_t B = mxGetM(prhs[1]), N = (size_t)c.N;
-    const double* x0 = in_matrix(prhs[1], B, 2, "x0");
-    mxArray* rho = mxCreateDoubleMatrix(B, 3 * N, mxREAL);
-    mxArray* uold = mxCreateDoubleMatrix(B, N, mxREAL);
+    const size_t B = mxGetN(prhs[1]), N = (size_t)c.N;
+    const double* x0 = in_matrix(prhs[1], 2, B, "x0");
+    mxArray* rho = mxCreateDoubleMatrix(3 * N, B, mxREAL);
+    mxArray* uold = mxCreateDoubleMatrix(N, B, mxREAL);
     check(ntm_mpc_init(ctx(), &p, &c, (int64_t)B, x0, mxGetDoubles(rho), mxGetDoubles(uold)), "ntm_mpc_init");
     plhs[0] = rho;
     if (nlhs > 1) plhs[1] = uold;
@@ -155,16 +160,16 @@ static void do_run(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     const ntm_config c = read_cfg(nrhs > 3 ? prhs[3] : NULL);
     ntm_physics p;
     ntm_physics_default(&p);
-    const size_t B = mxGetM(prhs[1]), N = (size_t)c.N;
-    const double* x0 = in_matrix(prhs[1], B, 2, "x0");
+    const size_t B = mxGetN(prhs[1]), N = (size_t)c.N;
+    const double* x0 = in_matrix(prhs[1], 2, B, "x0");
     const int k = (int)mxGetScalar(prhs[2]);
     if (k < 1) mexErrMsgIdAndTxt("ntm:arg", "k_sim must be >= 1");
-    mxArray* xk = mxCreateDoubleMatrix(B, 2 * (size_t)(k + 1), mxREAL);
-    mxArray* uk = mxCreateDoubleMatrix(B, (size_t)k, mxREAL);
-    mxArray* Uk = mxCreateDoubleMatrix(B, N * (size_t)k, mxREAL);
-    mxArray* wp = mxCreateDoubleMatrix(B, (N + 1) * (size_t)k, mxREAL);
-    mxArray* fl = mxCreateNumericMatrix(B, (size_t)k, mxINT32_CLASS, mxREAL);
-    mxArray* it = mxCreateNumericMatrix(B, (size_t)k, mxINT32_CLASS, mxREAL);
+    mxArray* xk = mxCreateDoubleMatrix(2 * (size_t)(k + 1), B, mxREAL);
+    mxArray* uk = mxCreateDoubleMatrix((size_t)k, B, mxREAL);
+    mxArray* Uk = mxCreateDoubleMatrix(N * (size_t)k, B, mxREAL);
+    mxArray* wp = mxCreateDoubleMatrix((N + 1) * (size_t)k, B, mxREAL);
+    mxArray* fl = mxCreateNumericMatrix((size_t)k, B, mxINT32_CLASS, mxREAL);
+    mxArray* it = mxCreateNumericMatrix((size_t)k, B, mxINT32_CLASS, mxREAL);
     check(ntm_mpc_run(ctx(), &p, &c, (int64_t)B, k, x0, mxGetDoubles(xk), mxGetDoubles(uk), mxGetDoubles(Uk),
                       mxGetDoubles(wp), mxGetInt32s(fl), mxGetInt32s(it)),
           "ntm_mpc_run");

@@ -808,17 +808,17 @@ struct StructRows {
 struct DenseRows {
     static constexpr bool kHasUnitRows = false;
     __device__ int unit_row(int, int, double& sg) const { sg = 0.0; return -1; }
-    const double* Lin;  // element (i, j) of scenario s at [(i + j*m)*B + s]
-    const double* b;    // [i*B + s]
+    const double* Lin;  // element (i, j) of scenario s at [s*m*N + i + j*m] (scenario-major)
+    const double* b;    // [s*m + i]
     double* rnrm;       // LDS, m entries
-    int64_t B, s;
+    int64_t nv, s;      // variables per scenario (N), scenario index
     int m;
 
     __device__ int rows() const { return m; }
     template <class W>
-    __device__ double lin(const W&, int i, int j) const { return Lin[((int64_t)i + (int64_t)j * m) * B + s]; }
+    __device__ double lin(const W&, int i, int j) const { return Lin[s * ((int64_t)m * nv) + i + (int64_t)j * m]; }
     template <class W>
-    __device__ double bval(const W&, int i) const { return b[(int64_t)i * B + s]; }
+    __device__ double bval(const W&, int i) const { return b[s * m + i]; }
     template <class W>
     __device__ double rnorm(const W&, int i) const { return rnrm[i]; }
 

@@ -32,15 +32,16 @@ template <int P, class W>
 __device__ __forceinline__ void load_state(const W& w, int64_t B, int64_t s, const double* rho,
                                            const double* U_old, int l) {
     const int N = w.n();
-    for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[(int64_t)e * B + s];
-    if (l < N) w.Uold()[l] = U_old[(int64_t)l * B + s];
+    const double* rs = rho + s * (3 * N);
+    for (int e = l; e < 3 * N; e += P) w.rho()[e] = rs[e];
+    if (l < N) w.Uold()[l] = U_old[s * N + l];
     NTM_WSYNC();
 }
 
 // XCD-aware block order (bijective): blocks are dealt round-robin over the 8
 // XCDs, so block b is given the k-th slot of XCD b%8's contiguous range of
-// scenario blocks.  Neighbouring scenarios share the cache lines of the SoA
-// (scenario-minor) state arrays; this keeps each line's users on one L2.
+// scenario blocks.  Neighbouring scenarios share the cache lines at the ends
+// of their (scenario-major) records; this keeps each line's users on one L2.
 __device__ __forceinline__ int64_t xcd_swizzle(int64_t b, int64_t nb) {
     const int64_t q = nb >> 3, r = nb & 7, x = b & 7, k = b >> 3;
     return x * q + (x < r ? x : r) + k;
@@ -55,7 +56,8 @@ template <int P, class W>
 __device__ void load_candidates(const Prob& pb, const W& w, int64_t B, int64_t s, const int32_t* ws, int l) {
     const int N = w.n();
     const int nrows = StructRows(pb).rows();
-    for (int e = l; e < 2 * (N + 1); e += P) w.cand()[e] = ws[(int64_t)e * B + s];
+    const int32_t* wss = ws + s * (2 * (N + 1));
+    for (int e = l; e < 2 * (N + 1); e += P) w.cand()[e] = wss[e];
     for (int i = l; i < nrows; i += P) w.aflag()[i] = 0;
     NTM_WSYNC();
     for (int slot = 0; slot < 2; ++slot) {
@@ -133,28 +135,30 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, 
     NTM_TRACE_SET(s, g, l);
     if (s >= B) return;
     auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
-    const double x0 = x_k[s], x1 = x_k[B + s];
+    const double x0 = x_k[2 * s], x1 = x_k[2 * s + 1];
     if (active_ws) load_candidates<P>(pb, w, B, s, active_ws, l);
     else if (l < 2) w.cand()[l * (N + 1) + N] = -1;
     load_state<P>(w, B, s, rho, U_old, l);
     int its;
     int flag = mpc_step_dev<P>(pb, w, x0, x1, l, &its, B, s);
-    for (int e = l; e < 3 * N; e += P) rho[(int64_t)e * B + s] = w.rho()[e];
+    // scenario-major outputs: each wave writes its scenario's contiguous records
+    for (int e = l; e < 3 * N; e += P) rho[s * (3 * N) + e] = w.rho()[e];
     if (l < N) {
-        U_old[(int64_t)l * B + s] = w.Uold()[l];
-        U[(int64_t)l * B + s] = w.U()[l];
+        U_old[s * N + l] = w.Uold()[l];
+        U[s * N + l] = w.U()[l];
     }
-    for (int e = l; e < 2 * (N + 1); e += P) x_pred[(int64_t)e * B + s] = w.xp()[e];
-    if (l == 0) {
+    for (int e = l; e < 2 * (N + 1); e += P) x_pred[s * (2 * (N + 1)) + e] = w.xp()[e];
+    if (l < 2) {
         double n0, n1;
         plant_step(pb, x0, x1, w.U()[0], n0, n1);
-        x_next[s] = n0;
-        x_next[B + s] = n1;
+        x_next[2 * s + l] = l ? n1 : n0;
+    }
+    if (l == 0) {
         exitflag[s] = flag;
         inner_iters[s] = its;
     }
     if (active_ws)
-        for (int e = l; e < 2 * (N + 1); e += P) active_ws[(int64_t)e * B + s] = w.cand()[e];
+        for (int e = l; e < 2 * (N + 1); e += P) active_ws[s * (2 * (N + 1)) + e] = w.cand()[e];
     NTM_STAMPS_FLUSH();
 }
 
@@ -169,7 +173,7 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_run(Prob pb, i
     const int N = NN > 0 ? NN : pb.N;
     if (s >= B) return;
     auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
-    double x0 = x0v[s], x1 = x0v[B + s];
+    double x0 = x0v[2 * s], x1 = x0v[2 * s + 1];
     if (l < 2) w.cand()[l * (N + 1) + N] = -1;
     {   // Rho = repmat(rho(x0), 1, N) (NTM_MPC_Sim.m:63-65); Uold = +inf (D14)
         double r1, r2, r3;
@@ -182,19 +186,19 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_run(Prob pb, i
         }
         NTM_WSYNC();
     }
-    if (xk && l == 0) { xk[s] = x0; xk[B + s] = x1; }
+    if (xk && l == 0) { xk[s * 2 * (k_sim + 1)] = x0; xk[s * 2 * (k_sim + 1) + 1] = x1; }
     for (int kk = 0; kk < k_sim; ++kk) {
         int its;
         int flag = mpc_step_dev<P>(pb, w, x0, x1, l, &its, B, s);
-        if (Uk && l < N) Uk[((int64_t)kk * N + l) * B + s] = w.U()[l];
-        if (wpred) for (int i = l; i <= N; i += P) wpred[((int64_t)kk * (N + 1) + i) * B + s] = w.xp()[2 * i];
+        if (Uk && l < N) Uk[(s * k_sim + kk) * N + l] = w.U()[l];
+        if (wpred) for (int i = l; i <= N; i += P) wpred[(s * k_sim + kk) * (N + 1) + i] = w.xp()[2 * i];
         double n0, n1;
         plant_step(pb, x0, x1, w.U()[0], n0, n1);
         if (l == 0) {
-            if (uk) uk[(int64_t)kk * B + s] = w.U()[0];
-            if (exitflag) exitflag[(int64_t)kk * B + s] = flag;
-            if (inner_iters) inner_iters[(int64_t)kk * B + s] = its;
-            if (xk) { xk[(int64_t)(2 * kk + 2) * B + s] = n0; xk[(int64_t)(2 * kk + 3) * B + s] = n1; }
+            if (uk) uk[s * k_sim + kk] = w.U()[0];
+            if (exitflag) exitflag[s * k_sim + kk] = flag;
+            if (inner_iters) inner_iters[s * k_sim + kk] = its;
+            if (xk) { xk[s * 2 * (k_sim + 1) + 2 * kk + 2] = n0; xk[s * 2 * (k_sim + 1) + 2 * kk + 3] = n1; }
         }
         x0 = n0;
         x1 = n1;
@@ -207,10 +211,10 @@ __global__ void k_rho(Prob pb, int64_t B, const double* x, double* rho) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= B) return;
     double r1, r2, r3;
-    rho_eval(pb.k, x[s], x[B + s], r1, r2, r3);
-    rho[s] = r1;
-    rho[B + s] = r2;
-    rho[2 * B + s] = r3;
+    rho_eval(pb.k, x[2 * s], x[2 * s + 1], r1, r2, r3);
+    rho[3 * s] = r1;
+    rho[3 * s + 1] = r2;
+    rho[3 * s + 2] = r3;
 }
 
 // initial LPV state: Rho = repmat(rho(x0), 1, N) (NTM_MPC_Sim.m:63-65), Uold = +Inf (D14)
@@ -218,25 +222,26 @@ __global__ void k_init_state(Prob pb, int64_t B, const double* x, double* rho, d
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= B) return;
     double r1, r2, r3;
-    rho_eval(pb.k, x[s], x[B + s], r1, r2, r3);
+    rho_eval(pb.k, x[2 * s], x[2 * s + 1], r1, r2, r3);
+    double* rs = rho + s * (3 * pb.N);
     for (int i = 0; i < pb.N; ++i) {
-        rho[(int64_t)(3 * i) * B + s] = r1;
-        rho[(int64_t)(3 * i + 1) * B + s] = r2;
-        rho[(int64_t)(3 * i + 2) * B + s] = r3;
-        U_old[(int64_t)i * B + s] = __builtin_inf();
+        rs[3 * i] = r1;
+        rs[3 * i + 1] = r2;
+        rs[3 * i + 2] = r3;
+        U_old[s * pb.N + i] = __builtin_inf();
     }
 }
 
 __global__ void k_AB(Prob pb, int64_t B, const double* rho, double* A, double* Bv) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= B) return;
-    double a11 = coef_a11(pb.k, rho[s]), a21 = coef_a21(pb.k, rho[B + s]), b = coef_b(pb.k, rho[2 * B + s]);
-    A[s] = a11;
-    A[B + s] = a21;
-    A[2 * B + s] = 0.0;
-    A[3 * B + s] = pb.k.a22;
-    Bv[s] = b;
-    Bv[B + s] = 0.0;
+    double a11 = coef_a11(pb.k, rho[3 * s]), a21 = coef_a21(pb.k, rho[3 * s + 1]), b = coef_b(pb.k, rho[3 * s + 2]);
+    A[4 * s] = a11;
+    A[4 * s + 1] = a21;
+    A[4 * s + 2] = 0.0;
+    A[4 * s + 3] = pb.k.a22;
+    Bv[2 * s] = b;
+    Bv[2 * s + 1] = 0.0;
 }
 
 template <int P, int NN>
@@ -249,21 +254,24 @@ __global__ __launch_bounds__(64) void k_lift(Prob pb, int64_t B, const double* r
     const int N = pb.N, R = 2 * N;
     if (s >= B) return;
     auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
-    for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[(int64_t)e * B + s];
+    for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[s * (3 * N) + e];
     NTM_WSYNC();
     lift_phase<P>(pb, w, l);
+    double* Phs = Phi + s * (4 * N);
+    double* Las = Lam + s * R;
     for (int i = l; i < N; i += P) {
         const double* Ph = w.Phi() + 4 * i;
-        Phi[(int64_t)(2 * i) * B + s] = Ph[0];
-        Phi[(int64_t)(2 * i + 1) * B + s] = Ph[1];
-        Phi[(int64_t)(R + 2 * i) * B + s] = Ph[2];
-        Phi[(int64_t)(R + 2 * i + 1) * B + s] = Ph[3];
-        Lam[(int64_t)(2 * i) * B + s] = w.Lam()[2 * i];
-        Lam[(int64_t)(2 * i + 1) * B + s] = w.Lam()[2 * i + 1];
+        Phs[2 * i] = Ph[0];
+        Phs[2 * i + 1] = Ph[1];
+        Phs[R + 2 * i] = Ph[2];
+        Phs[R + 2 * i + 1] = Ph[3];
+        Las[2 * i] = w.Lam()[2 * i];
+        Las[2 * i + 1] = w.Lam()[2 * i + 1];
     }
+    double* Gs = Gam + s * (R * N);
     for (int e = l; e < R * N; e += P) {
         int r = e % R, j = e / R;
-        Gam[(int64_t)e * B + s] = (r >= 2 * j) ? w.gt(r, j) : 0.0;
+        Gs[e] = (r >= 2 * j) ? w.gt(r, j) : 0.0;
     }
 }
 
@@ -277,18 +285,19 @@ __global__ __launch_bounds__(64) void k_cost(Prob pb, int64_t B, const double* r
     const int N = NN > 0 ? NN : pb.N;
     if (s >= B) return;
     auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
-    for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[(int64_t)e * B + s];
+    for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[s * (3 * N) + e];
     NTM_WSYNC();
     lift_phase<P>(pb, w, l);
-    free_response<P>(w, x[s], x[B + s], l);
+    free_response<P>(w, x[2 * s], x[2 * s + 1], l);
     cost_phase<P>(pb, w, l);
     if (l < N) {
+        double* Gs = G_out + s * (N * N);
         for (int kk = 0; kk <= l; ++kk) {
             double v = w.R()[l + kk * w.ldj()];
-            G_out[(int64_t)(l + kk * N) * B + s] = v;
-            G_out[(int64_t)(kk + l * N) * B + s] = v;
+            Gs[l + kk * N] = v;
+            Gs[kk + l * N] = v;
         }
-        F_out[(int64_t)l * B + s] = w.F()[l];
+        F_out[s * N + l] = w.F()[l];
     }
 }
 
@@ -303,16 +312,19 @@ __global__ __launch_bounds__(64) void k_getwlc(Prob pb, int64_t B, const double*
     const int N = pb.N, m = 6 * N + 4;
     if (s >= B) return;
     auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
-    for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[(int64_t)e * B + s];
+    for (int e = l; e < 3 * N; e += P) w.rho()[e] = rho[s * (3 * N) + e];
     NTM_WSYNC();
     lift_phase<P>(pb, w, l);
+    L += s * ((int64_t)m * N);
+    W += s * (2 * m);
+    c += s * m;
     for (int row = l; row < m; row += P) {
         int blk = row / 6, rr = row - 6 * blk;
         double Wr0 = 0.0, Wr1 = 0.0, cr = 0.0;
-        for (int j = 0; j < N; ++j) L[((int64_t)row + (int64_t)j * m) * B + s] = 0.0;
+        for (int j = 0; j < N; ++j) L[row + j * m] = 0.0;
         bool urow = blk < N && rr < 2;
         if (urow) {
-            L[((int64_t)row + (int64_t)blk * m) * B + s] = (rr == 0) ? -1.0 : 1.0;
+            L[row + blk * m] = (rr == 0) ? -1.0 : 1.0;
             cr = (rr == 0) ? -pb.umin : pb.umax;
         } else {
             int i, cc;
@@ -325,15 +337,15 @@ __global__ __launch_bounds__(64) void k_getwlc(Prob pb, int64_t B, const double*
                 if (cc == 0) Wr0 = -sg; else Wr1 = -sg;
             } else {
                 int r = 2 * (i - 1) + cc;
-                for (int j = 0; j < N; ++j) L[((int64_t)row + (int64_t)j * m) * B + s] = sg * ((r >= 2 * j) ? w.gt(r, j) : 0.0);
+                for (int j = 0; j < N; ++j) L[row + j * m] = sg * ((r >= 2 * j) ? w.gt(r, j) : 0.0);
                 Wr0 = -sg * w.Phi()[4 * (i - 1) + cc];
                 Wr1 = -sg * w.Phi()[4 * (i - 1) + 2 + cc];
                 cr -= sg * w.Lam()[r];
             }
         }
-        W[(int64_t)row * B + s] = Wr0;
-        W[(int64_t)(m + row) * B + s] = Wr1;
-        c[(int64_t)row * B + s] = cr;
+        W[row] = Wr0;
+        W[m + row] = Wr1;
+        c[row] = cr;
     }
 }
 
@@ -353,13 +365,13 @@ __global__ __launch_bounds__(64) void k_qp(int64_t B, int N, int m, const double
     double* rnrm = reinterpret_cast<double*>(base + ws_bytes(N));
     double* gsave = rnrm + ((m + 1) & ~1);     // copy of G~ for the polish (N x LDJ)
     if (l < N) {
-        for (int kk = 0; kk <= l; ++kk) w.R()[l + kk * w.ldj()] = G_in[((int64_t)l + (int64_t)kk * N) * B + s];
-        w.F()[l] = F_in[(int64_t)l * B + s];
+        for (int kk = 0; kk <= l; ++kk) w.R()[l + kk * w.ldj()] = G_in[s * (N * N) + l + kk * N];
+        w.F()[l] = F_in[s * N + l];
     }
     for (int i = l; i < m; i += P) w.aflag()[i] = 0;
     NTM_WSYNC();
     int flag, its = 0, q = 0;
-    DenseRows rows{Lin, b, rnrm, B, s, m};
+    DenseRows rows{Lin, b, rnrm, (int64_t)N, s, m};
     if (!scale_phase<P>(w, l, false)) {
         flag = NTM_EXIT_NONFINITE;
     } else {
@@ -379,7 +391,7 @@ __global__ __launch_bounds__(64) void k_qp(int64_t B, int N, int m, const double
         w.U()[l] = (flag == NTM_EXIT_MAXITER) ? w.V()[l] * w.D()[l] : 0.0;
     }
     NTM_WSYNC();
-    if (l < N) U[(int64_t)l * B + s] = w.U()[l];
+    if (l < N) U[s * N + l] = w.U()[l];
     if (l == 0) {
         exitflag[s] = flag;
         if (iters) iters[s] = its;
@@ -916,8 +928,8 @@ void ntm_scenarios_x0(uint64_t seed, int64_t first_id, int64_t B, double* x0) {
         uint64_t base = seed * 0x100000001B3ull + sid * 2;
         double u0 = (double)(splitmix64(base) >> 11) * (1.0 / 9007199254740992.0);
         double u1 = (double)(splitmix64(base + 1) >> 11) * (1.0 / 9007199254740992.0);
-        x0[k] = 0.07 + 0.07 * u0;
-        x0[B + k] = (0.8 + 0.4 * u1) * 2000 * pi;
+        x0[2 * k] = 0.07 + 0.07 * u0;
+        x0[2 * k + 1] = (0.8 + 0.4 * u1) * 2000 * pi;
     }
 }
 

@@ -14,7 +14,7 @@ LIB_PATH = Path(os.environ.get("NTM_MPC_LIB", PKG_ROOT / "lib" / "libntm_mpc.so"
 
 MAX_N = 64
 MODE_NONE, MODE_BOX, MODE_FULL, MODE_FULL_DU = 0, 1, 2, 3
-ABI_VERSION = 2          # include/ntm_mpc.h NTM_MPC_ABI_VERSION
+ABI_VERSION = 3          # include/ntm_mpc.h NTM_MPC_ABI_VERSION
 LITERAL_PHI_RIGHTMUL, LITERAL_GAMMA_INDEX, LITERAL_PLANT_NO_C, RHO1_SQUARED = 1, 2, 4, 8
 EXIT_OPTIMAL, EXIT_MAXITER, EXIT_INFEASIBLE, EXIT_NONFINITE = 1, 0, -2, -7
 NTM_OK = 0

@@ -14,17 +14,22 @@ meaning and error behaviour, batched over scenarios:
     NtmMpc.step                 NTM_MPC_Sim.m:94-130  (one time step, drop-in)
     NtmMpc.run / NTM_MPC_Sim    NTM_MPC_Sim.m:80-131  (closed loop)
 
-All batched tensors are torch fp64 CUDA tensors of shape (E, B) — element e
-of scenario s at [e, s], i.e. the C-ABI's scenario-minor SoA layout.  PyTorch
-is only plumbing (device memory, streams); every computation runs in the HIP
-kernels of lib/libntm_mpc.so.  There is no CPU fallback: without the library
-or a GPU, calls raise.
+All batched arrays have shape (E, B) — element e of scenario s at [e, s] —
+and their storage is the C-ABI's scenario-major layout: each scenario's
+E-record is contiguous, [s*E + e], i.e. the transpose of a contiguous (B, E)
+array (MATLAB's E-by-B arrays, one column per scenario).  Arrays this module
+returns are laid out that way, so passing them back costs nothing; any other
+(E, B) array is accepted too, through a staged copy (in/out arguments are
+copied back).  ``device_tensor`` builds a device tensor in the ABI layout from
+host data.  PyTorch is only plumbing (device memory, streams); every
+computation runs in the HIP kernels of lib/libntm_mpc.so.  There is no CPU
+fallback: without the library or a GPU, calls raise.
 """
 from __future__ import annotations
 
 import ctypes as C
 import math
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 
 import numpy as np
 import torch
@@ -101,6 +106,7 @@ def _ptr(t: torch.Tensor | None):
 
 
 def _check_dev(t: torch.Tensor, shape, dtype=torch.float64, name="tensor"):
+    """Plain contiguous CUDA array (instrumentation counters, SoA)."""
     if not isinstance(t, torch.Tensor) or not t.is_cuda:
         raise ValueError(f"{name} must be a CUDA tensor")
     if t.dtype != dtype:
@@ -109,6 +115,48 @@ def _check_dev(t: torch.Tensor, shape, dtype=torch.float64, name="tensor"):
         raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
     if not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
+
+
+def is_scenario_major(a) -> bool:
+    """(E, B) array whose storage is scenario-major ([s*E + e]); 1-D arrays trivially."""
+    if isinstance(a, np.ndarray):
+        return a.ndim < 2 or a.T.flags.c_contiguous
+    return a.dim() < 2 or a.T.is_contiguous()
+
+
+def _dev_arg(t, shape, dtype=torch.float64, name="tensor"):
+    """Validate an (E, B) CUDA argument; return (array in the ABI layout, staged?)."""
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ValueError(f"{name} must be a CUDA tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+    if is_scenario_major(t):
+        return t, False
+    return t.T.contiguous().T, True
+
+
+def _host_arg(a, shape, dtype=np.float64, name="array"):
+    """Validate an (E, B) host argument; return (array in the ABI layout, staged?)."""
+    if not isinstance(a, np.ndarray) or a.shape != tuple(shape) or a.dtype != dtype:
+        raise ValueError(f"{name}: expected {np.dtype(dtype).name} {tuple(shape)}")
+    if is_scenario_major(a):
+        return a, False
+    return np.asfortranarray(a), True
+
+
+def _host_empty(*shape, dtype=np.float64):
+    return np.empty(shape[::-1], dtype).T if len(shape) == 2 else np.empty(shape, dtype)
+
+
+def device_tensor(a, device=None, dtype=torch.float64) -> torch.Tensor:
+    """(E, B) host data -> (E, B) CUDA tensor in the ABI's scenario-major layout."""
+    a = np.asarray(a)
+    if device is None:
+        device = torch.cuda.current_device()
+    dev = device if isinstance(device, (str, torch.device)) else torch.device("cuda", int(device))
+    return torch.tensor(np.ascontiguousarray(a.T), dtype=dtype, device=dev).T
 
 
 class NtmMpc:
@@ -149,13 +197,21 @@ class NtmMpc:
             raise NtmLibraryError(f"{what} failed ({rc}): {self.lib.ntm_last_error(self._ctx).decode()}")
 
     def _empty(self, *shape, dtype=torch.float64):
-        return torch.empty(*shape, dtype=dtype, device=f"cuda:{self.device}")
+        """(E, B) output in the ABI's scenario-major layout (1-D: plain)."""
+        dev = f"cuda:{self.device}"
+        if len(shape) == 2:
+            return torch.empty(shape[1], shape[0], dtype=dtype, device=dev).T
+        return torch.empty(*shape, dtype=dtype, device=dev)
+
+    def tensor(self, a, dtype=torch.float64) -> torch.Tensor:
+        """(E, B) host data -> device tensor in the ABI layout on this controller's GPU."""
+        return device_tensor(a, self.device, dtype)
 
     def set_stats(self, stats: torch.Tensor | None):
-        """Accumulate per-scenario counters (NTM_STATS_ROWS=6, B) int32 into
-        ``stats`` during subsequent step/run launches: QP solves, GI iterations,
-        final active rows, state rows in the final active set, warm-start
-        candidate verifications, full GI solves; None disables."""
+        """Accumulate per-scenario counters (NTM_STATS_ROWS=6, B) int32 (plain
+        contiguous rows) into ``stats`` during subsequent step/run launches: QP
+        solves, GI iterations, final active rows, state rows in the final active
+        set, warm-start candidate verifications, full GI solves; None disables."""
         if stats is not None:
             if stats.dim() != 2 or stats.shape[0] != STATS_ROWS:
                 raise ValueError(f"stats must be ({STATS_ROWS}, B) int32")
@@ -174,7 +230,7 @@ class NtmMpc:
         """Rho = repmat(rho(x0), 1, N) (NTM_MPC_Sim.m:63-65); U_old = +inf (D14)."""
         cfg = cfg or self.config
         Bn = x0.shape[1]
-        _check_dev(x0, (2, Bn), name="x0")
+        x0, _ = _dev_arg(x0, (2, Bn), name="x0")
         rho, U_old = self._empty(3 * cfg.N, Bn), self._empty(cfg.N, Bn)
         self._raise(self.lib.ntm_mpc_init_device(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn,
                                                  _ptr(x0), _ptr(rho), _ptr(U_old), self._stream()),
@@ -185,9 +241,8 @@ class NtmMpc:
         """ntm_mpc_init with host arrays (the MEX path)."""
         cfg = cfg or self.config
         Bn = x0.shape[1]
-        if x0.shape != (2, Bn) or x0.dtype != np.float64 or not x0.flags.c_contiguous:
-            raise ValueError("x0: expected C-contiguous float64 (2, B)")
-        rho, U_old = np.empty((3 * cfg.N, Bn)), np.empty((cfg.N, Bn))
+        x0, _ = _host_arg(x0, (2, Bn), name="x0")
+        rho, U_old = _host_empty(3 * cfg.N, Bn), _host_empty(cfg.N, Bn)
         dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))          # noqa: E731
         self._raise(self.lib.ntm_mpc_init(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn,
                                           dp(x0), dp(rho), dp(U_old)), "ntm_mpc_init")
@@ -196,7 +251,7 @@ class NtmMpc:
     def new_active_ws(self, B: int, cfg: Config | None = None) -> torch.Tensor:
         """Empty warm-start workspace for step(..., active_ws=): (2(N+1), B) int32 of -1."""
         cfg = cfg or self.config
-        return torch.full((2 * (cfg.N + 1), B), -1, dtype=torch.int32, device=f"cuda:{self.device}")
+        return self._empty(2 * (cfg.N + 1), B, dtype=torch.int32).fill_(-1)
 
     def step(self, x_k: torch.Tensor, rho: torch.Tensor, U_old: torch.Tensor, cfg: Config | None = None,
              out: dict | None = None, active_ws: torch.Tensor | None = None):
@@ -204,22 +259,30 @@ class NtmMpc:
         ``U_old`` (N, B) are updated in place.  ``active_ws`` (see new_active_ws)
         carries the last two active sets from step to step as verified warm
         starts (ntm_mpc_step_ws_device).  Returns dict U, x_pred, x_next,
-        exitflag, inner_iters (all CUDA tensors)."""
+        exitflag, inner_iters (all CUDA tensors); ``out`` (a dict this method
+        returned earlier) is reused."""
         cfg = cfg or self.config
         N, Bn = cfg.N, x_k.shape[1]
-        _check_dev(x_k, (2, Bn), name="x_k")
-        _check_dev(rho, (3 * N, Bn), name="rho")
-        _check_dev(U_old, (N, Bn), name="U_old")
+        xk, _ = _dev_arg(x_k, (2, Bn), name="x_k")
+        rh, rho_st = _dev_arg(rho, (3 * N, Bn), name="rho")
+        uo, uo_st = _dev_arg(U_old, (N, Bn), name="U_old")
+        ws, ws_st = (None, False) if active_ws is None else _dev_arg(active_ws, (2 * (N + 1), Bn), torch.int32,
+                                                                     "active_ws")
         if out is None:
             out = {"U": self._empty(N, Bn), "x_pred": self._empty(2 * (N + 1), Bn), "x_next": self._empty(2, Bn),
                    "exitflag": self._empty(Bn, dtype=torch.int32), "inner_iters": self._empty(Bn, dtype=torch.int32)}
-        if active_ws is not None:
-            _check_dev(active_ws, (2 * (N + 1), Bn), dtype=torch.int32, name="active_ws")
+        else:
+            for k, shp in (("U", (N, Bn)), ("x_pred", (2 * (N + 1), Bn)), ("x_next", (2, Bn))):
+                if tuple(out[k].shape) != shp or not is_scenario_major(out[k]):
+                    raise ValueError(f"out[{k!r}] must be a {shp} array from an earlier step()")
         rc = self.lib.ntm_mpc_step_ws_device(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn,
-                                             _ptr(x_k), _ptr(rho), _ptr(U_old), _ptr(out["U"]), _ptr(out["x_pred"]),
+                                             _ptr(xk), _ptr(rh), _ptr(uo), _ptr(out["U"]), _ptr(out["x_pred"]),
                                              _ptr(out["x_next"]), _ptr(out["exitflag"]), _ptr(out["inner_iters"]),
-                                             _ptr(active_ws), self._stream())
+                                             _ptr(ws), self._stream())
         self._raise(rc, "ntm_mpc_step_ws_device")
+        for staged, dst, src in ((rho_st, rho, rh), (uo_st, U_old, uo), (ws_st, active_ws, ws)):
+            if staged:
+                dst.copy_(src)
         return out
 
     def run(self, x0: torch.Tensor, k_sim: int = 20, cfg: Config | None = None):
@@ -228,7 +291,7 @@ class NtmMpc:
         ((N+1) k_sim, B), exitflag / inner_iters (k_sim, B)."""
         cfg = cfg or self.config
         N, Bn = cfg.N, x0.shape[1]
-        _check_dev(x0, (2, Bn), name="x0")
+        x0, _ = _dev_arg(x0, (2, Bn), name="x0")
         out = {"xk": self._empty(2 * (k_sim + 1), Bn), "uk": self._empty(k_sim, Bn), "Uk": self._empty(N * k_sim, Bn),
                "wpred": self._empty((N + 1) * k_sim, Bn), "exitflag": self._empty(k_sim, Bn, dtype=torch.int32),
                "inner_iters": self._empty(k_sim, Bn, dtype=torch.int32)}
@@ -242,37 +305,37 @@ class NtmMpc:
     # ------------------------------------------------------------ host-buffer entry points (the MEX path)
     def step_host(self, x_k: np.ndarray, rho: np.ndarray, U_old: np.ndarray, cfg: Config | None = None,
                   active_ws: np.ndarray | None = None):
-        """ntm_mpc_step with host (NumPy, C-contiguous fp64) arrays, as a MEX
-        gateway calls it: the library stages through its own device buffers.
-        ``rho`` and ``U_old`` are updated in place."""
+        """ntm_mpc_step with host (NumPy fp64) arrays, as a MEX gateway calls it:
+        the library stages through its own device buffers.  ``rho`` and
+        ``U_old`` (and ``active_ws``) are updated in place."""
         cfg = cfg or self.config
         N, Bn = cfg.N, x_k.shape[1]
-        for a, shp, nm in ((x_k, (2, Bn), "x_k"), (rho, (3 * N, Bn), "rho"), (U_old, (N, Bn), "U_old")):
-            if a.shape != shp or a.dtype != np.float64 or not a.flags.c_contiguous:
-                raise ValueError(f"{nm}: expected C-contiguous float64 {shp}")
-        out = {"U": np.empty((N, Bn)), "x_pred": np.empty((2 * (N + 1), Bn)), "x_next": np.empty((2, Bn)),
+        xk, _ = _host_arg(x_k, (2, Bn), name="x_k")
+        rh, rho_st = _host_arg(rho, (3 * N, Bn), name="rho")
+        uo, uo_st = _host_arg(U_old, (N, Bn), name="U_old")
+        ws, ws_st = (None, False) if active_ws is None else _host_arg(active_ws, (2 * (N + 1), Bn), np.int32,
+                                                                      "active_ws")
+        out = {"U": _host_empty(N, Bn), "x_pred": _host_empty(2 * (N + 1), Bn), "x_next": _host_empty(2, Bn),
                "exitflag": np.empty(Bn, np.int32), "inner_iters": np.empty(Bn, np.int32)}
         dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))          # noqa: E731
         ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))           # noqa: E731
-        if active_ws is not None and (active_ws.shape != (2 * (N + 1), Bn) or active_ws.dtype != np.int32
-                                      or not active_ws.flags.c_contiguous):
-            raise ValueError(f"active_ws: expected C-contiguous int32 {(2 * (N + 1), Bn)}")
-        rc = self.lib.ntm_mpc_step_ws(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn, dp(x_k),
-                                      dp(rho), dp(U_old), dp(out["U"]), dp(out["x_pred"]), dp(out["x_next"]),
-                                      ip(out["exitflag"]), ip(out["inner_iters"]),
-                                      None if active_ws is None else ip(active_ws))
+        rc = self.lib.ntm_mpc_step_ws(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn, dp(xk),
+                                      dp(rh), dp(uo), dp(out["U"]), dp(out["x_pred"]), dp(out["x_next"]),
+                                      ip(out["exitflag"]), ip(out["inner_iters"]), None if ws is None else ip(ws))
         self._raise(rc, "ntm_mpc_step_ws")
+        for staged, dst, src in ((rho_st, rho, rh), (uo_st, U_old, uo), (ws_st, active_ws, ws)):
+            if staged:
+                dst[...] = src
         return out
 
     def run_host(self, x0: np.ndarray, k_sim: int = 20, cfg: Config | None = None):
         """ntm_mpc_run with host arrays (NTM_MPC_Sim.m:80-131 for a batch)."""
         cfg = cfg or self.config
         N, Bn = cfg.N, x0.shape[1]
-        if x0.shape != (2, Bn) or x0.dtype != np.float64 or not x0.flags.c_contiguous:
-            raise ValueError("x0: expected C-contiguous float64 (2, B)")
-        out = {"xk": np.empty((2 * (k_sim + 1), Bn)), "uk": np.empty((k_sim, Bn)), "Uk": np.empty((N * k_sim, Bn)),
-               "wpred": np.empty(((N + 1) * k_sim, Bn)), "exitflag": np.empty((k_sim, Bn), np.int32),
-               "inner_iters": np.empty((k_sim, Bn), np.int32)}
+        x0, _ = _host_arg(x0, (2, Bn), name="x0")
+        out = {"xk": _host_empty(2 * (k_sim + 1), Bn), "uk": _host_empty(k_sim, Bn),
+               "Uk": _host_empty(N * k_sim, Bn), "wpred": _host_empty((N + 1) * k_sim, Bn),
+               "exitflag": _host_empty(k_sim, Bn, dtype=np.int32), "inner_iters": _host_empty(k_sim, Bn, dtype=np.int32)}
         dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))          # noqa: E731
         ip = lambda a: a.ctypes.data_as(C.POINTER(C.c_int32))           # noqa: E731
         rc = self.lib.ntm_mpc_run(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn, k_sim, dp(x0),
@@ -285,7 +348,7 @@ class NtmMpc:
     def rho(self, x: torch.Tensor, cfg: Config | None = None):
         """rho1.m / rho2.m / rho3.m at x (2, B) -> (3, B)."""
         Bn = x.shape[1]
-        _check_dev(x, (2, Bn), name="x")
+        x, _ = _dev_arg(x, (2, Bn), name="x")
         out = self._empty(3, Bn)
         self._raise(self.lib.ntm_rho_device(self._ctx, C.byref(self.physics.to_c()), C.byref(self._cfg(cfg)), Bn,
                                             _ptr(x), _ptr(out), self._stream()), "ntm_rho_device")
@@ -294,7 +357,7 @@ class NtmMpc:
     def AB(self, rho: torch.Tensor, cfg: Config | None = None):
         """A.m / B.m at rho (3, B) -> A (4, B) col-major 2x2, B (2, B) column (D5)."""
         Bn = rho.shape[1]
-        _check_dev(rho, (3, Bn), name="rho")
+        rho, _ = _dev_arg(rho, (3, Bn), name="rho")
         A, Bv = self._empty(4, Bn), self._empty(2, Bn)
         self._raise(self.lib.ntm_AB_device(self._ctx, C.byref(self.physics.to_c()), C.byref(self._cfg(cfg)), Bn,
                                            _ptr(rho), _ptr(A), _ptr(Bv), self._stream()), "ntm_AB_device")
@@ -304,7 +367,7 @@ class NtmMpc:
         """Rho_to_PhiGammaLambda.m: rho (3N, B) -> Phi (4N, B), Gamma (2N*N, B), Lambda (2N, B)."""
         cfg = cfg or self.config
         N, Bn = cfg.N, rho.shape[1]
-        _check_dev(rho, (3 * N, Bn), name="rho")
+        rho, _ = _dev_arg(rho, (3 * N, Bn), name="rho")
         Phi, Gam, Lam = self._empty(4 * N, Bn), self._empty(2 * N * N, Bn), self._empty(2 * N, Bn)
         self._raise(self.lib.ntm_lift_device(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn,
                                              _ptr(rho), _ptr(Phi), _ptr(Gam), _ptr(Lam), self._stream()),
@@ -315,8 +378,8 @@ class NtmMpc:
         """NTM_MPC_Sim.m:120-121 -> G (N*N, B), F (N, B)."""
         cfg = cfg or self.config
         N, Bn = cfg.N, rho.shape[1]
-        _check_dev(rho, (3 * N, Bn), name="rho")
-        _check_dev(x_k, (2, Bn), name="x_k")
+        rho, _ = _dev_arg(rho, (3 * N, Bn), name="rho")
+        x_k, _ = _dev_arg(x_k, (2, Bn), name="x_k")
         G, F = self._empty(N * N, Bn), self._empty(N, Bn)
         self._raise(self.lib.ntm_cost_device(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn,
                                              _ptr(rho), _ptr(x_k), _ptr(G), _ptr(F), self._stream()),
@@ -328,7 +391,7 @@ class NtmMpc:
         cfg = cfg or self.config
         N, Bn = cfg.N, rho.shape[1]
         m = 6 * N + 4
-        _check_dev(rho, (3 * N, Bn), name="rho")
+        rho, _ = _dev_arg(rho, (3 * N, Bn), name="rho")
         W, Lm, c = self._empty(2 * m, Bn), self._empty(m * N, Bn), self._empty(m, Bn)
         self._raise(self.lib.ntm_getwlc_device(self._ctx, C.byref(self.physics.to_c()), C.byref(cfg.to_c()), Bn,
                                                _ptr(rho), _ptr(W), _ptr(Lm), _ptr(c), self._stream()),
@@ -342,11 +405,11 @@ class NtmMpc:
         (1 optimal, 0 max iterations, -2 infeasible -> U = 0, -7 non-finite)."""
         N, Bn = f.shape
         m = 0 if Lin is None else b.shape[0]
-        _check_dev(H, (N * N, Bn), name="H")
-        _check_dev(f, (N, Bn), name="f")
+        H, _ = _dev_arg(H, (N * N, Bn), name="H")
+        f, _ = _dev_arg(f, (N, Bn), name="f")
         if m:
-            _check_dev(Lin, (m * N, Bn), name="A")
-            _check_dev(b, (m, Bn), name="b")
+            Lin, _ = _dev_arg(Lin, (m * N, Bn), name="A")
+            b, _ = _dev_arg(b, (m, Bn), name="b")
         U = self._empty(N, Bn)
         flag = self._empty(Bn, dtype=torch.int32)
         its = self._empty(Bn, dtype=torch.int32)
@@ -357,9 +420,9 @@ class NtmMpc:
 
 
 def scenarios_x0(first_id: int, B: int, seed: int = 20241220):
-    """Synthetic initial states for global ids first_id..first_id+B-1, (2, B) float64 numpy."""
-    import numpy as np
-    x0 = np.empty((2, B), dtype=np.float64)
+    """Synthetic initial states for global ids first_id..first_id+B-1:
+    (2, B) float64 numpy array in the ABI layout (each scenario's [w, omega] contiguous)."""
+    x0 = _host_empty(2, B)
     L.load().ntm_scenarios_x0(C.c_uint64(seed), first_id, B, x0.ctypes.data_as(C.POINTER(C.c_double)))
     return x0
 
@@ -393,7 +456,7 @@ def rho3(x, w_dep=None):
 
 def Rho_to_PhiGammaLambda(Rho1, Rho2, Rho3, cfg: Config | None = None):
     """Rho_to_PhiGammaLambda.m (batched): Rho1/2/3 (N, B) -> Phi, Gamma, Lambda."""
-    rho = torch.stack([Rho1, Rho2, Rho3], dim=1).reshape(-1, Rho1.shape[1]).contiguous()
+    rho = torch.stack([Rho1, Rho2, Rho3], dim=1).reshape(-1, Rho1.shape[1])
     return _ctl().lift(rho, cfg)
 
 

@@ -1,8 +1,8 @@
 """ctypes binding of the C oracle (oracle/libntm_oracle.so) — TEST INFRASTRUCTURE ONLY.
 
 Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg only.
-Arrays use the same scenario-minor SoA layout as include/ntm_mpc.h:
-numpy arrays of shape (E, B), C-contiguous.
+Arrays are numpy (E, B) (element e of scenario s at [e, s]), staged C-contiguous
+(the oracle's own scenario-minor interface; any (E, B) array is accepted).
 """
 from __future__ import annotations
 

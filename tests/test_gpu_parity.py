@@ -411,7 +411,7 @@ def test_full_size_batch_properties(ctl, N, mode):
     import ntm_mpc
     B = 100_000
     cfg, ocfg = cfgs(N, mode)
-    x = torch.tensor(ntm_mpc.scenarios_x0(0, B), device=DEV)
+    x = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(0, B))
     rho, uo = ctl.initial_state(x, cfg)
     ws = ctl.new_active_ws(B, cfg)
     out = ctl.step(x, rho, uo, cfg, active_ws=ws)             # step 1 fills the workspace

@@ -10,7 +10,7 @@ cfg = Config(N=20, mode=2)
 ctl = NtmMpc(config=cfg)
 lib = ntm_mpc.load()
 buf = (C.c_ulonglong * 32)()
-x = torch.tensor(ntm_mpc.scenarios_x0(0, B), device="cuda")
+x = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(0, B))
 rho, uo = ctl.initial_state(x, cfg)
 ws = ctl.new_active_ws(B, cfg)
 out = ctl.step(x, rho, uo, cfg, active_ws=ws); torch.cuda.synchronize()

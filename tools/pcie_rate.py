@@ -19,15 +19,14 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 100000
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 cfg = Config(N=20, mode=2)
 ctl = NtmMpc(config=cfg)
-x = np.ascontiguousarray(ntm_mpc.scenarios_x0(0, B))
-rho_d, uo_d = ctl.initial_state(torch.tensor(x, device="cuda"), cfg)
-rho, uo = rho_d.cpu().numpy().copy(), uo_d.cpu().numpy().copy()
+x = ntm_mpc.scenarios_x0(0, B)                         # (2, B) in the ABI layout: no staging copies
+rho, uo = ctl.initial_state_host(x, cfg)
 out = ctl.step_host(x, rho, uo, cfg)                   # warmup
-x = np.ascontiguousarray(out["x_next"])
+x = out["x_next"]
 t = time.perf_counter()
 for _ in range(K):
     out = ctl.step_host(x, rho, uo, cfg)
-    x = np.ascontiguousarray(out["x_next"])
+    x = out["x_next"]
 dt = (time.perf_counter() - t) / K
 bytes_moved = B * 8 * (2 + 2 * 3 * 20 + 2 * 20 + 20 + 2 * 21 + 2) + B * 8
 print(json.dumps({"B": B, "steps": K, "ms_per_step": dt * 1e3, "steps_per_s": B / dt,

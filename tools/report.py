@@ -37,7 +37,7 @@ def main():
     cfg = Config(N=args.N, mode=args.mode)
     ctl = NtmMpc(config=cfg)
     B, K, N = args.scenarios, args.k_sim, args.N
-    x0 = torch.tensor(ntm_mpc.scenarios_x0(0, B), device="cuda")
+    x0 = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(0, B))
     out = ctl.run(x0, K, cfg)
     torch.cuda.synchronize()
     xk = out["xk"].cpu().numpy().reshape(K + 1, 2, B).transpose(2, 1, 0)       # (B, 2, K+1)

@@ -17,7 +17,7 @@ from ntm_mpc import Config, NtmMpc  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 100000
 cfg = Config(N=20, mode=2)
 ctl = NtmMpc(config=cfg)
-x = torch.tensor(ntm_mpc.scenarios_x0(0, B), device="cuda")
+x = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(0, B))
 rho, uo = ctl.initial_state(x, cfg)
 ws = ctl.new_active_ws(B, cfg)
 for _ in range(3):                                    # warm steps (advance the loop, fill the workspace)
