@@ -83,7 +83,7 @@ __shared__ int ntm_trace_grp;   // group (of this one-wave block) that owns the 
 // Diagnostic build only (-DNTM_STAMPS): per-phase s_memtime cycle totals,
 // summed over waves into ntm_stamps[] (read with ntm_debug_stamps).  The
 // production library compiles every stamp away.
-#define NTM_NSTAMPS 32
+#define NTM_NSTAMPS 40
 #ifdef NTM_STAMPS
 extern __device__ unsigned long long ntm_stamps[NTM_NSTAMPS];
 __shared__ unsigned long long ntm_lds_stamps[NTM_NSTAMPS];   // per block (= per wave), flushed once
@@ -110,7 +110,8 @@ __shared__ unsigned long long ntm_lds_stamps[NTM_NSTAMPS];   // per block (= per
 enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL, ST_GI_FACT, ST_GI_CHECK,
        ST_GI_DIR, ST_GI_ADD, ST_GI_DROP, CN_CHECK, CN_CAND, CN_HIT,
        ST_P_CLASS, ST_P_GRAM, ST_P_CHOL, ST_P_SCHUR, ST_P_BWD, ST_P_KKT, CN_REPAIR, CN_GIRUN,
-       ST_S_E, ST_S_Y, ST_S_K, ST_S_CHOL, ST_S_SOLVE, CN_TRY_EARLY, CN_FAIL_EARLY, CN_FAIL_LATE };
+       ST_S_E, ST_S_Y, ST_S_K, ST_S_CHOL, ST_S_SOLVE, CN_TRY_EARLY, CN_FAIL_EARLY, CN_FAIL_LATE,
+       CN_FAIL_IT1, CN_FAIL_IT2, CN_GI_IT1, CN_GI_IT2, CN_GI_LATE, CN_TRY_IT1, CN_TRY_IT2 };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 constexpr int kMaxNT = 32;         // explicit R^{-1} in GI up to this horizon (WS::useT)
 constexpr int kRepairs = 8;        // single-row repairs of a failed warm-start candidate
@@ -296,6 +297,7 @@ __device__ __forceinline__ double coef_b(const Coef& k, double r3) { return k.bc
 // unroll); NN == 0: runtime horizon (generic kernels).
 template <int NN>
 struct WS {
+    static constexpr int kNN = NN;
     int N_rt;
     double* base;
     __device__ __forceinline__ int n() const { return NN > 0 ? NN : N_rt; }
@@ -375,6 +377,67 @@ __device__ inline WS<NN> ws_carve(char* base, int N) {
     w.N_rt = N;
     w.base = reinterpret_cast<double*>(base);
     return w;
+}
+
+// ---------------------------------------------------------------------------
+// Batched LDS contractions.  The long masked fixed-trip loops below are LDS
+// latency chains when the scheduler interleaves each load with its use (the
+// 256-VGPR kernels leave it no room to hoist); these helpers issue CH rows of
+// loads, fence the scheduler, then consume them, so one LDS round trip serves
+// CH terms.  Same terms in the same order as the plain loops.  Loads of the
+// tail chunk past n are skipped (zero), never read out of the workspace.
+// ---------------------------------------------------------------------------
+// sum_{imin <= i < n} a_i' Q b_i over 2-vectors stored at stride 2
+template <int CH>
+__device__ __forceinline__ double qdot_rows(const double* a, const double* b, int n, int imin, double q00,
+                                            double q01, double q10, double q11) {
+    double s = 0.0;
+    for (int i0 = 0; i0 < n; i0 += CH) {
+        double a0[CH], a1[CH], b0[CH], b1[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int i = i0 + u;
+            const bool in = i < n;
+            a0[u] = in ? a[2 * i] : 0.0;
+            a1[u] = in ? a[2 * i + 1] : 0.0;
+            b0[u] = in ? b[2 * i] : 0.0;
+            b1[u] = in ? b[2 * i + 1] : 0.0;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int i = i0 + u;
+            const double o0 = q00 * b0[u] + q01 * b1[u];
+            const double o1 = q10 * b0[u] + q11 * b1[u];
+            const double t = a0[u] * o0 + a1[u] * o1;
+            s += (i >= imin && i < n) ? t : 0.0;
+        }
+    }
+    return s;
+}
+// Gamma_r v restricted to j <= r/2 (row r of the packed block-lower-triangular Gamma)
+template <int CH, class W>
+__device__ __forceinline__ double gamma_row_dot(const W& w, int r, const double* v) {
+    const int n = w.n(), jm = r >> 1;
+    const double* gr = w.Gt() + r;                        // gt(r, j) = gr[gidx(0, j)]
+    double y = 0.0;
+    for (int j0 = 0; j0 < n; j0 += CH) {
+        double g[CH], x[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int j = j0 + u;
+            const bool in = j < n;
+            g[u] = in ? gr[w.gidx(0, j)] : 0.0;
+            x[u] = in ? v[j] : 0.0;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int j = j0 + u;
+            y += (j <= jm ? g[u] : 0.0) * x[u];
+        }
+    }
+    return y;
 }
 
 // ---------------------------------------------------------------------------
@@ -1441,12 +1504,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
     //     next lift) and z = y_B + e - r (scratch in w.xp(), rewritten by the rollout) ---
     NTM_WSYNC();
     for (int r = l; r < 2 * N; r += P) {
-        const int jm = r >> 1;
-        double y = 0.0;
-        for (int j = 0; j < N; ++j) {
-            const double g = w.gt(r, j);
-            y += (j <= jm ? g : 0.0) * w.dr()[j];
-        }
+        const double y = gamma_row_dot<4>(w, r, w.dr());
         w.Phi()[r] = y;
         w.xp()[r] = y + w.e()[r] - ((r & 1) ? pb.r[1] : pb.r[0]);
     }
@@ -1457,15 +1515,22 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
     if (l < nF) {
         const int ja = w.fidx()[l];
         const double* ca = w.Gt() + w.gidx(2 * ja, ja) - 2 * ja;   // ca[r] = gt(r, ja), r >= 2 ja
-        double g2 = 0.0;
-        for (int i = 0; i < N; ++i) {                               // terms i < ja masked
-            const double z0 = w.xp()[2 * i], z1 = w.xp()[2 * i + 1];
-            const double t = ca[2 * i] * (q00 * z0 + q01 * z1) + ca[2 * i + 1] * (q10 * z0 + q11 * z1);
-            g2 += (i >= ja) ? t : 0.0;
-        }
+        const double g2 = qdot_rows<4>(ca, w.xp(), N, ja, q00, q01, q10, q11);   // terms i < ja masked
         gl = w.D()[ja] * (2 * g2);
     }
-    // --- compact G~_FF (lower, col-major in R): one (a, c) entry per lane ---
+    // Bordered KKT system (fused path): rows 0..nF-1 free variables, nF..nt-1 general
+    // rows, nt the right-hand side; kept packed row-major (row r at r(r+1)/2) in the
+    // contiguous J/R block.  Falls back to the two-stage Schur solve below when the
+    // bordered rows do not fit the group's lanes or the block.
+    const int nt = nF + nS;
+    // nt <= 2N (nS <= nF); a compile-time horizon whose worst case fits compiles the fused path only
+    constexpr int NNc = W::kNN, LDc = NNc | 1;
+    constexpr bool kAlwaysFused =
+        NNc > 0 && 2 * NNc + 1 <= P && (2 * NNc) * (2 * NNc + 1) / 2 + 2 * NNc <= NNc * LDc + (NNc + 1) * LDc;
+    const bool fused = kAlwaysFused || ((nt + 1 <= P) && (nt * (nt + 1) / 2 + nt <= N * LDJ + (N + 1) * LD));
+    double* const Lp = w.J();
+    if (fused && l < nF) Lp[(nt * (nt + 1)) / 2 + l] = -gl;
+    // --- compact G~_FF: one (a, c) entry per lane (packed rows, or lower col-major in R) ---
     {
         const int npair = nF * (nF + 1) / 2;
         for (int idx = l; idx < npair; idx += P) {
@@ -1476,15 +1541,10 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
             const int ja = w.fidx()[a], jc = w.fidx()[c];            // ja >= jc
             const double* ca = w.Gt() + w.gidx(2 * ja, ja) - 2 * ja;
             const double* cc = w.Gt() + w.gidx(2 * jc, jc) - 2 * jc;
-            double sg = 0.0;
-            for (int i = 0; i < N; ++i) {                            // terms i < ja masked
-                const double g0 = cc[2 * i], g1 = cc[2 * i + 1];
-                const double o0 = q00 * g0 + q01 * g1;
-                const double o1 = q10 * g0 + q11 * g1;
-                const double t = ca[2 * i] * o0 + ca[2 * i + 1] * o1;
-                sg += (i >= ja) ? t : 0.0;
-            }
-            w.R()[a + c * LD] = (2 * sg) * w.D()[ja] * w.D()[jc];
+            const double sg = qdot_rows<4>(ca, cc, N, ja, q00, q01, q10, q11);   // terms i < ja masked
+            const double gv = (2 * sg) * w.D()[ja] * w.D()[jc];
+            if (fused) Lp[idx] = gv;                                  // idx == a(a+1)/2 + c
+            else w.R()[a + c * LD] = gv;
         }
     }
     NTM_WSYNC();
@@ -1499,10 +1559,102 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
         }
         return (j <= (r >> 1)) ? -(((w.ssg()[s2] * w.gt(r, j)) * w.D()[j]) * w.irn()[r]) : 0.0;
     };
+    // h_s = n_s' V = bc_s - n_s,B' V_B with n_s,B' V_B = -sg irn_r (Gamma_r U_B)
+    auto hs_of = [&](int s2) -> double {
+        double hs = 0.0;
+        if (s2 < nS) {
+            const int r = w.srw()[s2];
+            const double sg = w.ssg()[s2];
+            if (r >= 2 * N) {                             // rate row i: b = du, fixed part sg (U_i - U_{i-1})
+                const int i = r - 2 * N;
+                const double ir = w.idun()[i];
+                const double ui = w.fx()[i] ? w.Uf()[i] : 0.0;
+                const double um = w.fx()[i - 1] ? w.Uf()[i - 1] : 0.0;
+                hs = -(rows.du * ir) + (sg * (ui - um)) * ir;
+            } else {
+                const int c = r & 1;
+                const double ir = w.irn()[r];
+                const double bval = (sg > 0.0) ? (rows.xmax(c) - w.e()[r]) : (-rows.xmin(c) + w.e()[r]);
+                hs = -(bval * ir) + (sg * w.Phi()[r]) * ir;
+            }
+        }
+        return hs;
+    };
     NTM_ACC(ST_P_GRAM, tp);
-    bool ok = !collide && chol_inplace<P>(w.R(), nF, 1, LD, l, w.ldi());
+    bool ok = !collide;
     int fk = ok ? 0 : 3, fpos_out = 0;
     double vfin = 0.0;
+    if (fused) {
+        // E rows over the free variables (one entry per lane) and h; the trailing
+        // block of A is zero and is never stored (the elimination starts it at 0)
+        for (int idx = l; idx < nF * nS; idx += P) {
+            const int s2 = idx / nF, a = idx - s2 * nF;
+            Lp[((nF + s2) * (nF + s2 + 1)) / 2 + a] = gen_n(s2, w.fidx()[a]);
+        }
+        if (l < nS) Lp[(nt * (nt + 1)) / 2 + nF + l] = hs_of(l);
+        NTM_WSYNC();
+        NTM_ACC(ST_S_E, tp);
+        // Left-looking elimination of A = [[G~_FF, E'], [E, 0]] = L_A diag(I, -I) L_A'
+        // over its nt columns: L_A = [[L, 0], [Y', L_K]] with L L' = G~_FF,
+        // Y = L^{-1} E', L_K L_K' = K = Y'Y (the Schur complement), in one pass
+        // whose right-hand-side row carries the forward substitution
+        // z = L_A^{-1} [-g_F; h].  Lane r owns row r.
+        double* const myrow = Lp + (l * (l + 1)) / 2;
+        if (ok) {
+            for (int k = 0; k < nt; ++k) {
+                const double* pk = Lp + (k * (k + 1)) / 2;
+                double sv = 0.0;
+                if (l >= k && l <= nt) {
+                    sv = (k >= nF && l < nt) ? 0.0 : myrow[k];
+                    // 4-way unrolled, masked: the loads of a chunk issue together
+                    // (reads past the row end stay inside the J/R/T block)
+                    const int kf = k < nF ? k : nF;
+                    for (int j = 0; j < kf; j += 4) {
+                        const double a0 = myrow[j], a1 = myrow[j + 1], a2 = myrow[j + 2], a3 = myrow[j + 3];
+                        const double b0 = pk[j], b1 = pk[j + 1], b2 = pk[j + 2], b3 = pk[j + 3];
+                        sv -= a0 * b0;
+                        sv -= (j + 1 < kf) ? a1 * b1 : 0.0;
+                        sv -= (j + 2 < kf) ? a2 * b2 : 0.0;
+                        sv -= (j + 3 < kf) ? a3 * b3 : 0.0;
+                    }
+                    for (int j = nF; j < k; j += 4) {
+                        const double a0 = myrow[j], a1 = myrow[j + 1], a2 = myrow[j + 2], a3 = myrow[j + 3];
+                        const double b0 = pk[j], b1 = pk[j + 1], b2 = pk[j + 2], b3 = pk[j + 3];
+                        sv += a0 * b0;
+                        sv += (j + 1 < k) ? a1 * b1 : 0.0;
+                        sv += (j + 2 < k) ? a2 * b2 : 0.0;
+                        sv += (j + 3 < k) ? a3 * b3 : 0.0;
+                    }
+                }
+                const double sk = (k < nF) ? sv : -sv;
+                const double dk = gbcast<P>(sk, k);
+                if (!(dk > 0.0) || !(dk < kInf)) { ok = false; fk = 3; break; }
+                const double il = rsqrt_nr(dk);
+                if (l > k && l <= nt) myrow[k] = sk * il;
+                if (l == k) { myrow[k] = dk * il; w.ldi()[k] = il; }   // ldi/kdi: 2N contiguous
+                NTM_WSYNC();
+            }
+        }
+        NTM_ACC(ST_S_CHOL, tp);
+        if (ok) {
+            // L_A' x = diag(I, -I) z: x = [V_F; -mu], one backward sweep.  The
+            // right-hand-side row holds sigma_k z_k (sigma = +1 free, -1 general
+            // columns), which is exactly diag(I, -I) z
+            double acc = (l < nt) ? Lp[(nt * (nt + 1)) / 2 + l] : 0.0, x = 0.0;
+            for (int k = nt - 1; k >= 0; --k) {
+                const double xk = gbcast<P>(acc, k) * w.ldi()[k];
+                if (l == k) x = xk;
+                if (l < k) acc -= Lp[(k * (k + 1)) / 2 + l] * xk;
+            }
+            if (l >= nF && l < nt) w.np()[l - nF] = -x;
+            NTM_WSYNC();
+            const double vsc = __shfl(x, (l < N && !fixed) ? fpos : 0, P);
+            vfin = fixed ? vb : vsc;
+        }
+        NTM_ACC(ST_S_SOLVE, tp);
+    } else if constexpr (!kAlwaysFused) {
+    ok = !collide && chol_inplace<P>(w.R(), nF, 1, LD, l, w.ldi());
+    fk = ok ? 0 : 3;
     if (ok) {
         const double wl = fwd_lanes<P>(w.R(), w.ldi(), nF, 1, LD, gl, l);    // L^{-1} g_F
         double tl = -wl;
@@ -1514,24 +1666,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
                 w.J()[a * LDJ + s2] = gen_n(s2, w.fidx()[a]);
             }
             if (l < nF) w.d()[l] = wl;
-            // h_s = n_s' V = bc_s - n_s,B' V_B with n_s,B' V_B = -sg irn_r (Gamma_r U_B)
-            double hs = 0.0;
-            if (l < nS) {
-                const int r = w.srw()[l];
-                const double sg = w.ssg()[l];
-                if (r >= 2 * N) {                         // rate row i: b = du, fixed part sg (U_i - U_{i-1})
-                    const int i = r - 2 * N;
-                    const double ir = w.idun()[i];
-                    const double ui = w.fx()[i] ? w.Uf()[i] : 0.0;
-                    const double um = w.fx()[i - 1] ? w.Uf()[i - 1] : 0.0;
-                    hs = -(rows.du * ir) + (sg * (ui - um)) * ir;
-                } else {
-                    const int c = r & 1;
-                    const double ir = w.irn()[r];
-                    const double bval = (sg > 0.0) ? (rows.xmax(c) - w.e()[r]) : (-rows.xmin(c) + w.e()[r]);
-                    hs = -(bval * ir) + (sg * w.Phi()[r]) * ir;
-                }
-            }
+            const double hs = hs_of(l);
             NTM_WSYNC();
             NTM_ACC(ST_S_E, tp);
             if (l < nS) {                          // Y = L^{-1} E': lane s solves column s
@@ -1586,21 +1721,14 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
             vfin = fixed ? vb : vsc;
         }
     }
+    }
     NTM_ACC(ST_P_BWD, tp);
     if (ok) {
         // ---- KKT certificate ----
         if (l < N) { w.V()[l] = vfin; w.U()[l] = w.D()[l] * vfin; }
         NTM_WSYNC();
         // y = Gamma U once, for the primal check (state rows) and the gradient
-        for (int r = l; r < 2 * N; r += P) {
-            const int jm = r >> 1;
-            double y = 0.0;
-            for (int j = 0; j < N; ++j) {
-                const double g = w.gt(r, j);
-                y += (j <= jm ? g : 0.0) * w.U()[j];
-            }
-            w.xp()[r] = y;
-        }
+        for (int r = l; r < 2 * N; r += P) w.xp()[r] = gamma_row_dot<4>(w, r, w.U());
         NTM_WSYNC();
         double vmax = gmax<P>(l < N ? fabs(vfin) : 0.0);
         Pick vf = rows.template check<P>(w, vfin, l, true, fmax(1.0, vmax), w.xp());
@@ -1609,12 +1737,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
         double res = 0.0;
         if (l < N) {
             const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;
-            double g2 = 0.0;
-            for (int i = 0; i < N; ++i) {                            // terms i < l masked
-                const double y0 = w.xp()[2 * i], y1 = w.xp()[2 * i + 1];
-                const double t = cl[2 * i] * (q00 * y0 + q01 * y1) + cl[2 * i + 1] * (q10 * y0 + q11 * y1);
-                g2 += (i >= l) ? t : 0.0;
-            }
+            const double g2 = qdot_rows<4>(cl, w.xp(), N, l, q00, q01, q10, q11);   // terms i < l masked
             res = w.D()[l] * (2 * g2) + w.F()[l];
             for (int s2 = 0; s2 < nS; ++s2) res -= w.np()[s2] * gen_n(s2, l);
         }
@@ -1706,6 +1829,60 @@ __device__ __forceinline__ void plant_step(const Prob& pb, double x0, double x1,
 }
 
 // ---------------------------------------------------------------------------
+// Receding-horizon shift of the carried warm-start set tried at inner
+// iteration 2 (start of an MPC step).  The previous step planned stages
+// k..k+N-1; this step plans k+1..k+N, so a row of stage i >= 1 moves to stage
+// i-1, stage-0 rows are dropped, and the bound rows of the old last input are
+// kept for the new last input as well.  Iteration 1 keeps its set unshifted:
+// its QP still runs on the previous step's (unshifted, D20) scheduling
+// parameters, and measured on MI355X (B=1e5, N=20) shifting that set doubles
+// its GI fallbacks, while shifting the iteration-2 set cuts them by a third.
+// Only a hint: every candidate is re-solved exactly and KKT-certified.
+// ---------------------------------------------------------------------------
+template <int P, class W>
+__device__ void shift_candidates(const Prob& pb, const W& w, int l) {
+    const int N = w.n();
+    if (pb.mode == NTM_MODE_NONE) return;
+    const int lane = threadIdx.x & 63;
+    const unsigned long long gmask = (P == 64) ? ~0ull : (((1ull << P) - 1ull) << (lane & ~(P - 1)));
+    const unsigned long long below = (1ull << lane) - 1ull;
+    {
+        int* c = w.cand() + (N + 1);                           // slot 1: tried at iteration 2
+        const int q = uni<P>(c[N]);
+        if (q <= 0) return;
+        int nid = -1, dup = -1;
+        if (l < q) {
+            const int id = c[l];
+            if (pb.mode == NTM_MODE_BOX) {
+                const int j = id < N ? id : id - N;
+                if (j >= 1) nid = id - 1;
+                if (j == N - 1) dup = id;
+            } else if (id >= 6 * N + 4) {                    // rate row of input j
+                const int j = ((id - (6 * N + 4)) >> 1) + 1;
+                if (j >= 2) nid = id - 2;
+                if (j == N - 1) dup = id;
+            } else if (id >= 6 * N) {                        // terminal state row -> stage N-1
+                nid = 6 * (N - 1) + 2 + (id - 6 * N);
+            } else {
+                const int blk = id / 6, rr = id - 6 * blk;
+                if (blk >= 1) nid = id - 6;
+                if (blk == N - 1 && rr < 2) dup = id;
+            }
+        }
+        NTM_WSYNC();
+        const unsigned long long bk = __ballot(nid >= 0) & gmask;
+        const unsigned long long bd = __ballot(dup >= 0) & gmask;
+        const int nk = uni<P>((int)__popcll(bk)), nd = uni<P>((int)__popcll(bd));
+        const bool with_dup = nk + nd <= N;
+        if (nid >= 0) c[__popcll(bk & below)] = nid;
+        if (with_dup && dup >= 0) c[nk + __popcll(bd & below)] = dup;
+        NTM_WSYNC();
+        if (l == 0) c[N] = nk + (with_dup ? nd : 0);
+        NTM_WSYNC();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // one inner iteration's QP: build -> scale -> GI -> polish -> w.U()
 // ---------------------------------------------------------------------------
 template <int P, class W>
@@ -1759,6 +1936,8 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                     if (rep == 0) {
                         if (it <= 2) NTM_CNT(CN_TRY_EARLY);
                         if (!okc) { if (it <= 2) NTM_CNT(CN_FAIL_EARLY); else NTM_CNT(CN_FAIL_LATE); }
+                        if (it == 1) { NTM_CNT(CN_TRY_IT1); if (!okc) NTM_CNT(CN_FAIL_IT1); }
+                        if (it == 2) { NTM_CNT(CN_TRY_IT2); if (!okc) NTM_CNT(CN_FAIL_IT2); }
                     }
                     if (okc) {
                         flag = NTM_EXIT_OPTIMAL;
@@ -1807,6 +1986,7 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                     NTM_ACC(ST_REGRAM, tq);
                     if (n_girun) ++*n_girun;
                     NTM_CNT(CN_GIRUN);
+                    if (it == 1) NTM_CNT(CN_GI_IT1); else if (it == 2) NTM_CNT(CN_GI_IT2); else NTM_CNT(CN_GI_LATE);
                     flag = gi_solve<P, StructRows, W>(w, rows, pb.mode != NTM_MODE_NONE, nrows, l,
                                                       qp_iters, &q);
                     NTM_ACC(ST_GI, tq);

@@ -501,7 +501,7 @@ static int orc_polish(int n, int m, const double* Gs, const double* Fs, const do
 static int orc_qp(int n, int m, const double* G, const double* F, const double* Lin,
                   const double* b, double* U, int* iters_out) {
     static __thread double Gs[NMAX * NMAX], Ls[MMAX * NMAX];
-    double D[NMAX], Fs[NMAX], bs[MMAX], V[NMAX];
+    double D[NMAX], Fs[NMAX] = {0}, bs[MMAX] = {0}, V[NMAX];
     for (int j = 0; j < n; ++j) {
         double g = G[(size_t)j * n + j];
         D[j] = (g > 0.0) ? 1.0 / sqrt(g) : 1.0;

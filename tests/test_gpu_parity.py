@@ -28,6 +28,9 @@ U_TOL = 1e-10
 # restatements differ by up to 8.4e-9 umax and each sits within ~4e-9 umax of a
 # 30-digit solve of the same active set, so the per-step bound is 5e-8 umax
 U_TOL_RATE = 5e-8
+# predicted / next states, relative to |w| ~ 0.15 m and |omega| ~ 2000 pi: 1e-9 in
+# modes 0-2; mode 3 scales with U_TOL_RATE (the states are rollouts of U), 1e-8
+X_TOL, X_TOL_RATE = 1e-9, 1e-8
 
 
 def T(a):
@@ -215,10 +218,11 @@ def test_step_teacher_forced(ctl, N, mode, warm):
         cmp = same if mode == 3 else np.ones_like(same)
         worst = max(worst, np.max(np.abs(H(out["U"]) - ref["U"])[:, cmp], initial=0.0) / cfg.umax)
         xn = H(out["x_next"])
-        assert np.max(np.abs(xn - ref["x_next"])[:, cmp] / xscale, initial=0.0) <= 1e-9
+        xtol = X_TOL_RATE if mode == 3 else X_TOL
+        assert np.max(np.abs(xn - ref["x_next"])[:, cmp] / xscale, initial=0.0) <= xtol
         xp = H(out["x_pred"]).reshape(N + 1, 2, -1).transpose(1, 0, 2)
         xr = ref["x_pred"].reshape(N + 1, 2, -1).transpose(1, 0, 2)
-        assert np.max(np.abs(xp - xr)[:, :, cmp] / xscale[:, :, None], initial=0.0) <= 1e-9
+        assert np.max(np.abs(xp - xr)[:, :, cmp] / xscale[:, :, None], initial=0.0) <= xtol
         x, rho, Uo = ref["x_next"], ref["rho"], ref["U_old"]
     assert worst <= (U_TOL_RATE if mode == 3 else (U_TOL if N <= 20 else 1e-8)), worst
     assert same_iters >= 0.9 * n, (same_iters, n)
