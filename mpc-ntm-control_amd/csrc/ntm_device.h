@@ -415,6 +415,25 @@ __device__ __forceinline__ double qdot_rows(const double* a, const double* b, in
     }
     return s;
 }
+// sum_{j < n} a[j sa] b[j sb] (strided LDS vectors)
+template <int CH>
+__device__ __forceinline__ double dot_batched(const double* a, int sa, const double* b, int sb, int n) {
+    double y = 0.0;
+    for (int j0 = 0; j0 < n; j0 += CH) {
+        double x[CH], z[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int j = j0 + u;
+            const bool in = j < n;
+            x[u] = in ? a[j * sa] : 0.0;
+            z[u] = in ? b[j * sb] : 0.0;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) y += x[u] * z[u];
+    }
+    return y;
+}
 // Gamma_r v restricted to j <= r/2 (row r of the packed block-lower-triangular Gamma)
 template <int CH, class W>
 __device__ __forceinline__ double gamma_row_dot(const W& w, int r, const double* v) {
@@ -586,16 +605,33 @@ __device__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_st
         const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
         const double r0 = pb.r[0], r1 = pb.r[1];
         double s = 0.0, fs = 0.0;
-        for (int i = 0; i < N; ++i) {            // fixed trip count, terms i < l masked
-            const double g0 = cj[2 * i], g1 = cj[2 * i + 1];
-            const double o0 = q00 * g0 + q01 * g1;
-            const double o1 = q10 * g0 + q11 * g1;
-            const double t = g0 * o0 + g1 * o1;
-            const double e0 = w.e()[2 * i] - r0, e1 = w.e()[2 * i + 1] - r1;
-            const double tf = g0 * (q00 * e0 + q01 * e1) + g1 * (q10 * e0 + q11 * e1);
-            if (i >= l) bad |= !isfinite(g0) || !isfinite(g1);
-            s += (i >= l) ? t : 0.0;
-            fs += (i >= l) ? tf : 0.0;
+        constexpr int CH = 4;
+        for (int i0 = 0; i0 < N; i0 += CH) {     // fixed trip count, terms i < l masked; batched loads
+            double ga[CH], gb[CH], ea[CH], eb[CH];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int i = i0 + u;
+                const bool in = i < N;
+                ga[u] = in ? cj[2 * i] : 0.0;
+                gb[u] = in ? cj[2 * i + 1] : 0.0;
+                ea[u] = in ? w.e()[2 * i] : 0.0;
+                eb[u] = in ? w.e()[2 * i + 1] : 0.0;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int i = i0 + u;
+                const double g0 = ga[u], g1 = gb[u];
+                const double o0 = q00 * g0 + q01 * g1;
+                const double o1 = q10 * g0 + q11 * g1;
+                const double t = g0 * o0 + g1 * o1;
+                const double e0 = ea[u] - r0, e1 = eb[u] - r1;
+                const double tf = g0 * (q00 * e0 + q01 * e1) + g1 * (q10 * e0 + q11 * e1);
+                const bool on = i >= l && i < N;
+                if (on) bad |= !isfinite(g0) || !isfinite(g1);
+                s += on ? t : 0.0;
+                fs += on ? tf : 0.0;
+            }
         }
         double g = 2 * s;
         double Dl = (g > 0.0 && g < kInf) ? rsqrt_nr(g) : 1.0;
@@ -616,9 +652,21 @@ __device__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_st
         for (int r = l; r < 2 * N; r += P) {
             double s = 0.0;
             const int jmax = r >> 1;
-            for (int j = 0; j < N; ++j) {        // fixed trip count, j > jmax masked
-                const double v = w.gt(r, j) * w.D()[j];
-                s += (j <= jmax) ? v * v : 0.0;
+            constexpr int CH = 4;
+            for (int j0 = 0; j0 < N; j0 += CH) { // fixed trip count, j > jmax masked; batched loads
+                double g[CH], dd[CH];
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    const int j = j0 + u;
+                    g[u] = j < N ? w.gt(r, j) : 0.0;
+                    dd[u] = j < N ? w.D()[j] : 0.0;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    const double v = g[u] * dd[u];
+                    s += (j0 + u <= jmax) ? v * v : 0.0;
+                }
             }
             bad |= !isfinite(s) || !isfinite(w.e()[r]);
             const double ir = (s > 0.0 && s < kInf) ? rsqrt_nr(s) : 0.0;
@@ -826,12 +874,10 @@ struct StructRows {
                     if (y_pre) {
                         xh = y_pre[r];
                     } else {
-                        // fixed trip count (unrolls); entries j > jmax are masked.  The packed
-                        // reads stay inside Gt: gidx(0, j) + r = j(2N-j-1) + r < N(N+1)
-                        for (int j = 0; j < N; ++j) {
-                            const double g = gr[w.gidx(0, j)];
-                            xh += (j <= jmax ? g : 0.0) * w.U()[j];
-                        }
+                        // fixed trip count, entries j > jmax masked.  The packed reads stay
+                        // inside Gt: gidx(0, j) + r = j(2N-j-1) + r < N(N+1)
+                        (void)gr;
+                        xh = gamma_row_dot<4>(w, r, w.U());
                     }
                     const double er = w.e()[r];
                     xh += er;
