@@ -1647,37 +1647,66 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
         // z = L_A^{-1} [-g_F; h].  Lane r owns row r.
         double* const myrow = Lp + (l * (l + 1)) / 2;
         if (ok) {
-            for (int k = 0; k < nt; ++k) {
-                const double* pk = Lp + (k * (k + 1)) / 2;
-                double sv = 0.0;
-                if (l >= k && l <= nt) {
-                    sv = (k >= nF && l < nt) ? 0.0 : myrow[k];
-                    // 4-way unrolled, masked: the loads of a chunk issue together
-                    // (reads past the row end stay inside the J/R/T block)
+            // blocks of KB columns: one pass of loads over the finished columns j < k
+            // serves all KB pivot rows, then the block's own triangle is finished in
+            // registers (L[k+b, k+c] broadcast from lane k+b).  Each column still
+            // accumulates its terms in column order, as the unblocked elimination.
+            constexpr int KB = 4;
+            for (int k = 0; k < nt; k += KB) {
+                const int kb = (nt - k < KB) ? nt - k : KB;
+                const bool live = l >= k && l <= nt;
+                double sacc[KB];
+#pragma unroll
+                for (int b2 = 0; b2 < KB; ++b2) {
+                    const int col = k + b2;
+                    sacc[b2] = (b2 < kb && live && l >= col) ? ((col >= nF && l < nt) ? 0.0 : myrow[col]) : 0.0;
+                }
+                if (live) {
                     const int kf = k < nF ? k : nF;
-                    for (int j = 0; j < kf; j += 4) {
-                        const double a0 = myrow[j], a1 = myrow[j + 1], a2 = myrow[j + 2], a3 = myrow[j + 3];
-                        const double b0 = pk[j], b1 = pk[j + 1], b2 = pk[j + 2], b3 = pk[j + 3];
-                        sv -= a0 * b0;
-                        sv -= (j + 1 < kf) ? a1 * b1 : 0.0;
-                        sv -= (j + 2 < kf) ? a2 * b2 : 0.0;
-                        sv -= (j + 3 < kf) ? a3 * b3 : 0.0;
-                    }
-                    for (int j = nF; j < k; j += 4) {
-                        const double a0 = myrow[j], a1 = myrow[j + 1], a2 = myrow[j + 2], a3 = myrow[j + 3];
-                        const double b0 = pk[j], b1 = pk[j + 1], b2 = pk[j + 2], b3 = pk[j + 3];
-                        sv += a0 * b0;
-                        sv += (j + 1 < k) ? a1 * b1 : 0.0;
-                        sv += (j + 2 < k) ? a2 * b2 : 0.0;
-                        sv += (j + 3 < k) ? a3 * b3 : 0.0;
+                    for (int j = 0; j < k; j += 2) {
+                        const bool in1 = j + 1 < k;
+                        const double a0 = myrow[j], a1 = in1 ? myrow[j + 1] : 0.0;
+                        double p0[KB], p1[KB];
+#pragma unroll
+                        for (int b2 = 0; b2 < KB; ++b2) {
+                            const double* pr = Lp + ((k + b2) * (k + b2 + 1)) / 2;
+                            p0[b2] = (b2 < kb) ? pr[j] : 0.0;
+                            p1[b2] = (b2 < kb && in1) ? pr[j + 1] : 0.0;
+                        }
+                        const double s0 = (j < kf) ? -1.0 : 1.0, s1 = (j + 1 < kf) ? -1.0 : 1.0;
+#pragma unroll
+                        for (int b2 = 0; b2 < KB; ++b2) {
+                            sacc[b2] += (s0 * a0) * p0[b2];
+                            sacc[b2] += in1 ? (s1 * a1) * p1[b2] : 0.0;
+                        }
                     }
                 }
-                const double sk = (k < nF) ? sv : -sv;
-                const double dk = gbcast<P>(sk, k);
-                if (!(dk > 0.0) || !(dk < kInf)) { ok = false; fk = 3; break; }
-                const double il = rsqrt_nr(dk);
-                if (l > k && l <= nt) myrow[k] = sk * il;
-                if (l == k) { myrow[k] = dk * il; w.ldi()[k] = il; }   // ldi/kdi: 2N contiguous
+                double Lc[KB];
+#pragma unroll
+                for (int b2 = 0; b2 < KB; ++b2) {
+                    Lc[b2] = 0.0;
+                    if (b2 < kb) {
+                        const int col = k + b2;
+#pragma unroll
+                        for (int c = 0; c < b2; ++c) {           // block columns k..col-1, in order
+                            const double lkc = gbcast<P>(Lc[c], col);   // L[col, k+c] from lane col
+                            const double sc = (k + c < nF) ? -1.0 : 1.0;
+                            sacc[b2] += (sc * Lc[c]) * lkc;
+                        }
+                        const double sk = (col < nF) ? sacc[b2] : -sacc[b2];
+                        const double dk = gbcast<P>(sk, col);
+                        if (!(dk > 0.0) || !(dk < kInf)) { ok = false; fk = 3; }
+                        else {
+                            const double il = rsqrt_nr(dk);
+                            Lc[b2] = (l == col) ? dk * il : sk * il;
+                            if (l == col) w.ldi()[col] = il;          // ldi/kdi: 2N contiguous
+                        }
+                    }
+                }
+                if (!ok) break;
+#pragma unroll
+                for (int b2 = 0; b2 < KB; ++b2)
+                    if (b2 < kb && l >= k + b2 && l <= nt) myrow[k + b2] = Lc[b2];
                 NTM_WSYNC();
             }
         }
