@@ -38,6 +38,21 @@ __device__ __forceinline__ void load_state(const W& w, int64_t B, int64_t s, con
     NTM_WSYNC();
 }
 
+__device__ __forceinline__ bool is16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// One scenario's record of n doubles from LDS to HBM.  With a 16-byte aligned
+// destination and an even n, lanes store two doubles each (16-B stores: every
+// request carries whole 16-B granules); otherwise one double per lane.
+template <int P>
+__device__ __forceinline__ void store_record(double* dst, const double* src, int n, int l) {
+    if (is16(dst) && (n & 1) == 0) {
+        for (int e = 2 * l; e < n; e += 2 * P)
+            *reinterpret_cast<double2*>(dst + e) = make_double2(src[e], src[e + 1]);
+    } else {
+        for (int e = l; e < n; e += P) dst[e] = src[e];
+    }
+}
+
 // XCD-aware block order (bijective): blocks are dealt round-robin over the 8
 // XCDs, so block b is given the k-th slot of XCD b%8's contiguous range of
 // scenario blocks.  Neighbouring scenarios share the cache lines at the ends
@@ -146,16 +161,18 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, 
     int its;
     int flag = mpc_step_dev<P>(pb, w, x0, x1, l, &its, B, s);
     // scenario-major outputs: each wave writes its scenario's contiguous records
-    for (int e = l; e < 3 * N; e += P) rho[s * (3 * N) + e] = w.rho()[e];
-    if (l < N) {
-        U_old[s * N + l] = w.Uold()[l];
-        U[s * N + l] = w.U()[l];
-    }
-    for (int e = l; e < 2 * (N + 1); e += P) x_pred[s * (2 * (N + 1)) + e] = w.xp()[e];
-    if (l < 2) {
+    store_record<P>(rho + s * (3 * N), w.rho(), 3 * N, l);
+    store_record<P>(U_old + s * N, w.Uold(), N, l);
+    store_record<P>(U + s * N, w.U(), N, l);
+    store_record<P>(x_pred + s * (2 * (N + 1)), w.xp(), 2 * (N + 1), l);
+    {
         double n0, n1;
         plant_step(pb, x0, x1, w.U()[0], n0, n1);
-        x_next[2 * s + l] = l ? n1 : n0;
+        if (is16(x_next)) {
+            if (l == 0) *reinterpret_cast<double2*>(x_next + 2 * s) = make_double2(n0, n1);
+        } else if (l < 2) {
+            x_next[2 * s + l] = l ? n1 : n0;
+        }
     }
     if (l == 0) {
         exitflag[s] = flag;

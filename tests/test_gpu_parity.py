@@ -307,15 +307,23 @@ def test_run_closed_loop(ctl, N, mode):
 
 
 def test_step_matches_run_first_step(ctl):
-    """ntm_mpc_run's first step == ntm_mpc_step from the same initial state."""
+    """ntm_mpc_run's first step == ntm_mpc_step from the same initial state.
+
+    The two are separate kernels built from the same device phases; the compiler
+    may contract a*b+c into FMAs differently in each, so they agree to rounding
+    (same exit flags and inner iterations, U and x_next to 1e-12 relative), not
+    necessarily bit for bit."""
     N, B = 20, 16
     cfg, ocfg = cfgs(N, 2)
     x0 = O.scenario_x0(np.arange(B)).T
     rho, Uo = ctl.initial_state(T(x0), cfg)
     st = ctl.step(T(x0), rho, Uo, cfg)
     rn = ctl.run(T(x0), 1, cfg)
-    assert torch.equal(st["U"][0], rn["uk"][0])
-    assert torch.equal(st["x_next"], rn["xk"][2:4])
+    assert torch.equal(st["exitflag"], rn["exitflag"][0])
+    assert torch.equal(st["inner_iters"], rn["inner_iters"][0])
+    assert torch.max(torch.abs(st["U"][0] - rn["uk"][0])).item() <= 1e-12 * cfg.umax
+    xs = torch.tensor([[0.15], [2000 * math.pi]], dtype=torch.float64, device=DEV)
+    assert torch.max(torch.abs(st["x_next"] - rn["xk"][2:4]) / xs).item() <= 1e-12
 
 
 @pytest.mark.gpu
