@@ -472,25 +472,38 @@ __device__ void lift_phase(const Prob& pb, const W& w, int l) {
         w.bb()[l] = coef_b(k, w.rho()[3 * l + 2]);
     }
     NTM_WSYNC();
-    // Gamma: lane j owns column j: Gamma_jj = B_j, Gamma_ij = A_i Gamma_{i-1,j} (D6)
-    if (l < N) {
-        double* col = w.Gt() + w.gidx(2 * l, l) - 2 * l;   // col[r], r >= 2l
-        double g0 = w.bb()[l], g1 = 0.0;
-        col[2 * l] = g0;
-        col[2 * l + 1] = g1;
+    // Gamma: lane j owns column j: Gamma_jj = B_j, Gamma_ij = A_i Gamma_{i-1,j} (D6).
+    // Lanes N and N+1 run the same 2-vector recursion for the two columns of
+    // Phi_i = A_i Phi_{i-1} (D4), lane N+2 for Lambda_i = A_i Lambda_{i-1} + C,
+    // all in the one loop (the group has the idle lanes for N + 3 <= P).
+    const bool extra = N + 3 <= P;
+    if (l < N || (extra && l < N + 3)) {
+        const bool gam = l < N;
+        const int ph = l - N;                          // 0, 1: Phi column; 2: Lambda
+        double g0, g1;
+        if (gam) { g0 = w.bb()[l]; g1 = 0.0; }
+        else if (ph == 0) { g0 = w.a11()[0]; g1 = w.a21()[0]; }
+        else if (ph == 1) { g0 = 0.0; g1 = k.a22; }
+        else { g0 = k.C1; g1 = k.C2; }
+        const double c0 = (ph == 2) ? k.C1 : 0.0, c1 = (ph == 2) ? k.C2 : 0.0;
+        double* col = w.Gt() + w.gidx(2 * l, l) - 2 * l;   // col[r], r >= 2l (Gamma lanes)
+        auto put = [&](int i) {
+            if (gam) { col[2 * i] = g0; col[2 * i + 1] = g1; }
+            else if (ph < 2) { w.Phi()[4 * i + 2 * ph] = g0; w.Phi()[4 * i + 2 * ph + 1] = g1; }
+            else { w.Lam()[2 * i] = g0; w.Lam()[2 * i + 1] = g1; }
+        };
+        put(gam ? l : 0);
         for (int i = 1; i < N; ++i) {        // fixed trip count (unrolls), branch-free:
-            const double n0 = w.a11()[i] * g0;   // rows i <= l keep (B_l, 0) and rewrite
-            const double n1 = w.a21()[i] * g0 + k.a22 * g1;   // the column's own diagonal
-            const bool live = i > l;
+            const double n0 = w.a11()[i] * g0 + c0;        // Gamma rows i <= l keep (B_l, 0)
+            const double n1 = (w.a21()[i] * g0 + k.a22 * g1) + c1;   // and rewrite the diagonal
+            const bool live = !gam || i > l;
             g0 = live ? n0 : g0;
             g1 = live ? n1 : g1;
-            const int ii = live ? i : l;
-            col[2 * ii] = g0;
-            col[2 * ii + 1] = g1;
+            put(live ? i : l);
         }
     }
-    // Phi (left-multiplied, D4) and Lambda: short sequential chains on lane 0
-    if (l == 0) {
+    // Phi and Lambda on lane 0 when the group has no idle lanes
+    if (!extra && l == 0) {
         double p00 = w.a11()[0], p10 = w.a21()[0], p01 = 0.0, p11 = k.a22;
         double l0 = k.C1, l1 = k.C2;
         w.Phi()[0] = p00; w.Phi()[1] = p10; w.Phi()[2] = p01; w.Phi()[3] = p11;
