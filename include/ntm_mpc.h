@@ -102,7 +102,7 @@ const char* ntm_last_error(const ntm_ctx* ctx);
  * 5 full Goldfarb-Idnani solves.  NULL disables. */
 #define NTM_STATS_ROWS 6
 int ntm_ctx_set_stats(ntm_ctx* ctx, int32_t* dev_stats);
-/* Diagnostic builds only: per-phase s_memtime cycle totals (32 counters);
+/* Diagnostic builds only: per-phase s_memtime cycle totals (48 counters);
  * NTM_E_UNSUPPORTED in production builds. */
 int ntm_debug_stamps(unsigned long long* out32, int reset);
 /* Launch shape the step/run kernels use for horizon N: lanes per scenario

@@ -83,7 +83,7 @@ __shared__ int ntm_trace_grp;   // group (of this one-wave block) that owns the 
 // Diagnostic build only (-DNTM_STAMPS): per-phase s_memtime cycle totals,
 // summed over waves into ntm_stamps[] (read with ntm_debug_stamps).  The
 // production library compiles every stamp away.
-#define NTM_NSTAMPS 40
+#define NTM_NSTAMPS 48
 #ifdef NTM_STAMPS
 extern __device__ unsigned long long ntm_stamps[NTM_NSTAMPS];
 __shared__ unsigned long long ntm_lds_stamps[NTM_NSTAMPS];   // per block (= per wave), flushed once
@@ -111,10 +111,11 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        ST_GI_DIR, ST_GI_ADD, ST_GI_DROP, CN_CHECK, CN_CAND, CN_HIT,
        ST_P_CLASS, ST_P_GRAM, ST_P_CHOL, ST_P_SCHUR, ST_P_BWD, ST_P_KKT, CN_REPAIR, CN_GIRUN,
        ST_S_E, ST_S_Y, ST_S_K, ST_S_CHOL, ST_S_SOLVE, CN_TRY_EARLY, CN_FAIL_EARLY, CN_FAIL_LATE,
-       CN_FAIL_IT1, CN_FAIL_IT2, CN_GI_IT1, CN_GI_IT2, CN_GI_LATE, CN_TRY_IT1, CN_TRY_IT2 };
+       CN_FAIL_IT1, CN_FAIL_IT2, CN_GI_IT1, CN_GI_IT2, CN_GI_LATE, CN_TRY_IT1, CN_TRY_IT2, CN_WARM_TRY, CN_WARM_OK, CN_WARM_DEP, CN_WARM_NEG, CN_WARM_FULL };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 constexpr int kMaxNT = 32;         // explicit R^{-1} in GI up to this horizon (WS::useT)
 constexpr int kRepairs = 8;        // single-row repairs of a failed warm-start candidate
+constexpr int kGiWarmRejected = 100;   // gi_solve: the warm-start set was not dual feasible (caller reruns cold)
 
 #define NTM_WSYNC()                                              \
     do {                                                         \
@@ -1054,7 +1055,8 @@ __device__ double bwd_lanes(const double* L, const double* rdiag, int n, int RS,
 // (Goldfarb & Idnani 1983, section 3).
 // ---------------------------------------------------------------------------
 template <int P, class Rows, class W>
-__device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, int l, int* iters_out, int* q_out) {
+__device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, int l, int* iters_out, int* q_out,
+                        int nwarm = 0) {
     const int N = w.n(), LD = w.ldj(), LDJ = w.ldj();
     *iters_out = 0;
     *q_out = 0;
@@ -1096,6 +1098,122 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
     if (useT && l < N) for (int b = 0; b < N; ++b) w.T()[l * LDJ + b] = 0.0;
     const int max_iter = 10 * (N + nrows) + 50;
     int q = 0, it = 0;
+    // Warm start (explicit T only): the rows w.sidx()[0..nwarm) of a failed
+    // candidate are added first without primal steps (Householder on J, R and T
+    // gain their columns), then V is set to the equality-constrained optimum on
+    // that set, V = -J2 J2' F~ + J1 T' bc, with multipliers u = T (T' bc + J1' F~).
+    // Rows dependent on those already added are skipped (a failed candidate often
+    // holds a state row and a bound row that fix the same variable).  If every
+    // u >= 0 the pair satisfies GI's invariant (optimal for the active set, dual
+    // feasible) and the iteration continues from it; otherwise the caller
+    // re-forms G~ and runs GI cold.
+    if (nwarm > 0 && useT && has_rows) {
+        NTM_CNT(CN_WARM_TRY);
+        bool okw = true;
+        for (int a = 0; a < nwarm; ++a) {
+            const int p = uni<P>(w.sidx()[a]);
+            int ej = -1;
+            double esg = 0.0, bcp, dl = 0.0;
+            if constexpr (Rows::kHasUnitRows) {
+                ej = uni<P>(rows.unit_row(p, N, esg));
+                esg = uni<P>(esg);
+            }
+            if (ej >= 0) {                        // u-bound row: n_p = -+e_j, d = J' n_p a signed row of J
+                bcp = uni<P>(-(rows.bval(w, p) / rows.rnorm(w, p)));
+                if (l < N) dl = esg * w.J()[ej * LDJ + l];
+            } else {
+                bcp = uni<P>(rows.template load_np<P>(w, p, l));
+                if (l < N) for (int i = 0; i < N; ++i) dl += w.J()[i * LDJ + l] * w.np()[i];
+            }
+            if (l < N) { w.d()[l] = (l >= q) ? dl : 0.0; w.dr()[l] = (l < q) ? dl : 0.0; }
+            NTM_WSYNC();
+            double rl = 0.0;
+            if (l < N) {
+#pragma unroll 4
+                for (int b = 0; b < N; ++b) rl += w.T()[l * LDJ + b] * w.dr()[b];
+            }
+            const double zn = gsum<P>((l >= q && l < N) ? dl * dl : 0.0);
+            const double dnrm = gsum<P>(dl * dl);
+            if (q >= N) { NTM_CNT(CN_WARM_FULL); break; }
+            if (zn <= 1e-300 || zn <= (kDepTol * kDepTol) * dnrm) {   // dependent on the rows added: skip it
+                NTM_CNT(CN_WARM_DEP);
+                NTM_WSYNC();
+                continue;
+            }
+            const double nrm = sqrt(zn);
+            const double dqv = gbcast<P>(dl, q);
+            double h = dqv;
+            if (q < N - 1) {
+                h = (dqv >= 0.0) ? -nrm : nrm;
+                double vl = (l == q) ? dl - h : ((l > q && l < N) ? dl : 0.0);
+                if (l < N) w.hv()[l] = vl;
+                double vtv = gsum<P>(vl * vl);
+                NTM_WSYNC();
+                if (l < N) {
+                    double dot = 0.0;
+                    for (int k2 = 0; k2 < N; ++k2) dot += w.J()[l * LDJ + k2] * w.hv()[k2];
+                    double f = 2.0 * dot / vtv;
+                    for (int k2 = q; k2 < N; ++k2) w.J()[l * LDJ + k2] -= f * w.hv()[k2];
+                }
+            }
+            const double ih = 1.0 / h;
+            if (l < q) {
+                w.R()[l + q * LD] = dl;
+                w.T()[l * LDJ + q] = -rl * ih;
+            }
+            if (l == q) {
+                w.R()[q + q * LD] = h;
+                w.T()[q * LDJ + q] = ih;
+                w.act()[q] = p;
+                w.aflag()[p] = kActiveRow;
+                w.Vb()[q] = bcp;                     // bc of active row q (scratch)
+            }
+            ++q;
+            NTM_WSYNC();
+        }
+        if (okw) {
+            // c = J' F~ (lane k), wv = (T' bc)_k for k < q
+            double c = 0.0, wv = 0.0;
+            if (l < N) for (int i = 0; i < N; ++i) c += w.J()[i * LDJ + l] * w.F()[i];
+            if (l < q) for (int a2 = 0; a2 <= l; ++a2) wv += w.T()[a2 * LDJ + l] * w.Vb()[a2];
+            if (l < N) {
+                w.d()[l] = (l >= q) ? c : 0.0;
+                w.dr()[l] = (l < q) ? wv : 0.0;
+                w.np()[l] = (l < q) ? wv + c : 0.0;
+            }
+            NTM_WSYNC();
+            double v = 0.0, u = 0.0;
+            if (l < N) for (int k2 = 0; k2 < N; ++k2) v += w.J()[l * LDJ + k2] * (w.dr()[k2] - w.d()[k2]);
+            if (l < q) for (int b = l; b < q; ++b) u += w.T()[l * LDJ + b] * w.np()[b];
+            const double uabs = gmax<P>(l < q ? fabs(u) : 0.0);
+            const double umin = -gmax<P>(l < q ? -u : -kInf);
+            okw = !(umin < -1e-9 * fmax(1.0, uabs)) && gmaxi<P>((l < N && !isfinite(v)) ? 1 : 0) == 0;
+            if (!okw) {
+                NTM_CNT(CN_WARM_NEG);
+                // the added rows whose multipliers are >= 0: the caller's second warm pass
+                const int lane = threadIdx.x & 63;
+                const unsigned long long gm = (P == 64) ? ~0ull : (((1ull << P) - 1ull) << (lane & ~(P - 1)));
+                const bool keep = l < q && u >= 0.0;
+                const unsigned long long bk = __ballot(keep) & gm;
+                const int id = (l < q) ? w.act()[l] : 0;
+                NTM_WSYNC();
+                if (keep) w.sidx()[__popcll(bk & ((1ull << lane) - 1ull))] = id;
+                *q_out = uni<P>((int)__popcll(bk));
+            }
+            if (okw) {
+                Vl = (l < N) ? v : 0.0;
+                if (l < N) { w.V()[l] = Vl; w.U()[l] = w.D()[l] * Vl; }
+                if (l < q) w.uu()[l] = fmax(0.0, u);
+                NTM_CNT(CN_WARM_OK);
+            }
+            NTM_WSYNC();
+        }
+        if (!okw) {
+            if (l < q) w.aflag()[w.act()[l]] = kCandRow;   // back to steering flags
+            NTM_WSYNC();
+            return kGiWarmRejected;                        // *q_out: rows kept in w.sidx() (0: none)
+        }
+    }
     for (;;) {
         const double vmax = gmax<P>(l < N ? fabs(Vl) : 0.0);
         Pick pk = rows.template check<P>(w, Vl, l, false, fmax(1.0, vmax));
@@ -2001,6 +2119,7 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
         } else {
             NTM_ACC(ST_SCALE, tq);
             bool done = false;
+            int nwarm = 0;
             // warm start: the LPV loop alternates between two QPs (a 2-cycle),
             // so the active set of iteration it-2 is tried first; it is taken
             // only if the exact active-set solve passes the KKT certificate
@@ -2061,8 +2180,13 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                     NTM_WSYNC();
                 }
                 if (!done) {
-                    // the repaired set steers GI's add order (StructRows::check)
-                    if (l < cq) w.aflag()[w.act()[l]] = kCandRow;
+                    // the repaired set steers GI's add order (StructRows::check) and,
+                    // with the explicit T, is GI's warm-start set (gi_solve)
+                    if (l < cq) {
+                        w.aflag()[w.act()[l]] = kCandRow;
+                        w.sidx()[l] = w.act()[l];
+                    }
+                    nwarm = cq;
                     NTM_WSYNC();
                 }
                 NTM_ACC(ST_CAND, tq);
@@ -2075,8 +2199,16 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                     if (n_girun) ++*n_girun;
                     NTM_CNT(CN_GIRUN);
                     if (it == 1) NTM_CNT(CN_GI_IT1); else if (it == 2) NTM_CNT(CN_GI_IT2); else NTM_CNT(CN_GI_LATE);
-                    flag = gi_solve<P, StructRows, W>(w, rows, pb.mode != NTM_MODE_NONE, nrows, l,
-                                                      qp_iters, &q);
+                    // one inlined GI: warm from the failed candidate; if its multipliers are
+                    // not all >= 0, warm again from the rows whose multipliers were; then cold
+                    for (int pass = 0;; ++pass) {
+                        flag = gi_solve<P, StructRows, W>(w, rows, pb.mode != NTM_MODE_NONE, nrows, l,
+                                                          qp_iters, &q, pass < 2 ? nwarm : 0);
+                        if (flag != kGiWarmRejected) break;
+                        nwarm = (pass == 0) ? q : 0;
+                        q = 0;
+                        if (!full_gram<P>(pb, w, l)) { flag = NTM_EXIT_NONFINITE; break; }
+                    }
                     NTM_ACC(ST_GI, tq);
                     if (flag == NTM_EXIT_OPTIMAL) {
                         const bool okp = polish_compact<P>(pb, w, rows, q, l, false, &ns);

@@ -9,7 +9,7 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
 cfg = Config(N=20, mode=2)
 ctl = NtmMpc(config=cfg)
 lib = ntm_mpc.load()
-buf = (C.c_ulonglong * 40)()
+buf = (C.c_ulonglong * 48)()
 x = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(0, B))
 rho, uo = ctl.initial_state(x, cfg)
 ws = ctl.new_active_ws(B, cfg)
@@ -37,3 +37,5 @@ for i, n in enumerate(sch):
     print(f"    {n:9s} {buf[24 + i]/B:12.0f}")
 print(f"per wave-step: tries it=1 {buf[37]/B:.2f} failed {buf[32]/B:.2f}; tries it=2 {buf[38]/B:.2f} failed {buf[33]/B:.2f}; "
       f"GI solves at it=1 {buf[34]/B:.2f}, it=2 {buf[35]/B:.2f}, later {buf[36]/B:.2f}")
+print(f"per wave-step: GI warm starts tried {buf[39]/B:.2f}, accepted {buf[40]/B:.2f}")
+print(f"  dependent rows skipped {buf[41]/B:.3f}; rejected: negative multiplier {buf[42]/B:.3f}; stopped at N rows {buf[43]/B:.3f}")
