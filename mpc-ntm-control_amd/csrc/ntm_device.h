@@ -1098,16 +1098,18 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
     if (useT && l < N) for (int b = 0; b < N; ++b) w.T()[l * LDJ + b] = 0.0;
     const int max_iter = 10 * (N + nrows) + 50;
     int q = 0, it = 0;
-    // Warm start (explicit T only): the rows w.sidx()[0..nwarm) of a failed
+    // Warm start: the rows w.sidx()[0..nwarm) of a failed
     // candidate are added first without primal steps (Householder on J, R and T
     // gain their columns), then V is set to the equality-constrained optimum on
-    // that set, V = -J2 J2' F~ + J1 T' bc, with multipliers u = T (T' bc + J1' F~).
+    // that set, V = -J2 J2' F~ + J1 R^{-T} bc, with multipliers
+    // u = R^{-1} (R^{-T} bc + J1' F~) (matvecs with T = R^{-1} for N <= 32,
+    // triangular solves on R above).
     // Rows dependent on those already added are skipped (a failed candidate often
     // holds a state row and a bound row that fix the same variable).  If every
     // u >= 0 the pair satisfies GI's invariant (optimal for the active set, dual
     // feasible) and the iteration continues from it; otherwise the caller
     // re-forms G~ and runs GI cold.
-    if (nwarm > 0 && useT && has_rows) {
+    if (nwarm > 0 && has_rows) {
         NTM_CNT(CN_WARM_TRY);
         bool okw = true;
         for (int a = 0; a < nwarm; ++a) {
@@ -1128,7 +1130,7 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
             if (l < N) { w.d()[l] = (l >= q) ? dl : 0.0; w.dr()[l] = (l < q) ? dl : 0.0; }
             NTM_WSYNC();
             double rl = 0.0;
-            if (l < N) {
+            if (useT && l < N) {
 #pragma unroll 4
                 for (int b = 0; b < N; ++b) rl += w.T()[l * LDJ + b] * w.dr()[b];
             }
@@ -1159,11 +1161,11 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
             const double ih = 1.0 / h;
             if (l < q) {
                 w.R()[l + q * LD] = dl;
-                w.T()[l * LDJ + q] = -rl * ih;
+                if (useT) w.T()[l * LDJ + q] = -rl * ih;
             }
             if (l == q) {
                 w.R()[q + q * LD] = h;
-                w.T()[q * LDJ + q] = ih;
+                if (useT) w.T()[q * LDJ + q] = ih;
                 w.act()[q] = p;
                 w.aflag()[p] = kActiveRow;
                 w.Vb()[q] = bcp;                     // bc of active row q (scratch)
@@ -1175,7 +1177,16 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
             // c = J' F~ (lane k), wv = (T' bc)_k for k < q
             double c = 0.0, wv = 0.0;
             if (l < N) for (int i = 0; i < N; ++i) c += w.J()[i * LDJ + l] * w.F()[i];
-            if (l < q) for (int a2 = 0; a2 <= l; ++a2) wv += w.T()[a2 * LDJ + l] * w.Vb()[a2];
+            if (useT) {
+                if (l < q) for (int a2 = 0; a2 <= l; ++a2) wv += w.T()[a2 * LDJ + l] * w.Vb()[a2];
+            } else {                                 // long horizons: R' wv = bc by forward substitution
+                double acc = (l < q) ? w.Vb()[l] : 0.0;
+                for (int k2 = 0; k2 < q; ++k2) {
+                    const double xk = gbcast<P>(acc, k2) / w.R()[k2 + k2 * LD];
+                    if (l == k2) wv = xk;
+                    if (l > k2 && l < q) acc -= w.R()[k2 + l * LD] * xk;
+                }
+            }
             if (l < N) {
                 w.d()[l] = (l >= q) ? c : 0.0;
                 w.dr()[l] = (l < q) ? wv : 0.0;
@@ -1184,7 +1195,16 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
             NTM_WSYNC();
             double v = 0.0, u = 0.0;
             if (l < N) for (int k2 = 0; k2 < N; ++k2) v += w.J()[l * LDJ + k2] * (w.dr()[k2] - w.d()[k2]);
-            if (l < q) for (int b = l; b < q; ++b) u += w.T()[l * LDJ + b] * w.np()[b];
+            if (useT) {
+                if (l < q) for (int b = l; b < q; ++b) u += w.T()[l * LDJ + b] * w.np()[b];
+            } else {                                 // R u = wv + c1 by back substitution
+                double acc = (l < q) ? w.np()[l] : 0.0;
+                for (int b = q - 1; b >= 0; --b) {
+                    const double ub = gbcast<P>(acc, b) / w.R()[b + b * LD];
+                    if (l == b) u = ub;
+                    if (l < b) acc -= w.R()[l + b * LD] * ub;
+                }
+            }
             const double uabs = gmax<P>(l < q ? fabs(u) : 0.0);
             const double umin = -gmax<P>(l < q ? -u : -kInf);
             okw = !(umin < -1e-9 * fmax(1.0, uabs)) && gmaxi<P>((l < N && !isfinite(v)) ? 1 : 0) == 0;
@@ -2181,7 +2201,7 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                 }
                 if (!done) {
                     // the repaired set steers GI's add order (StructRows::check) and,
-                    // with the explicit T, is GI's warm-start set (gi_solve)
+                    // is GI's warm-start set (gi_solve)
                     if (l < cq) {
                         w.aflag()[w.act()[l]] = kCandRow;
                         w.sidx()[l] = w.act()[l];
