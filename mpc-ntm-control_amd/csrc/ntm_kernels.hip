@@ -106,14 +106,6 @@ __device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x
     int n_qp = 0, n_gi = 0, n_act = 0, n_gen = 0, n_try = 0, n_girun = 0;
     for (it = 1; it <= pb.i_sim; ++it) {
         int qi = 0, qa = 0, ns = 0;
-#ifdef NTM_OPAQUE_LANE
-        // diagnostic variant (make nospill): an opaque copy of the lane index, so
-        // lane-derived LDS addresses are rebuilt per iteration instead of hoisted
-        // out of the loop and spilled (profiles/README.md, Traffic)
-        const int l_out = l;
-        int l = l_out;
-        if constexpr (W::kNN > 0 && W::kNN <= 32) asm volatile("" : "+v"(l));
-#endif
         flag = qp_phase<P>(pb, w, x0, x1, l, &qi, &qa, &ns, (it - 1) & 1, &n_try, &n_girun, it);
         ++n_qp;
         n_gi += qi;
