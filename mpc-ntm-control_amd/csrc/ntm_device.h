@@ -1814,15 +1814,22 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
                 }
                 if (live) {
                     const int kf = k < nF ? k : nF;
+                    // unconditional loads (no branch per load): j + 1 <= k stays inside row l
+                    // (l >= k) and row k+b2; pivot rows past the block clamp to row nt
+                    const double* prb[KB];
+#pragma unroll
+                    for (int b2 = 0; b2 < KB; ++b2) {
+                        const int rr = (k + b2 < nt) ? k + b2 : nt;
+                        prb[b2] = Lp + (rr * (rr + 1)) / 2;
+                    }
                     for (int j = 0; j < k; j += 2) {
                         const bool in1 = j + 1 < k;
-                        const double a0 = myrow[j], a1 = in1 ? myrow[j + 1] : 0.0;
+                        const double a0 = myrow[j], a1 = myrow[j + 1];
                         double p0[KB], p1[KB];
 #pragma unroll
                         for (int b2 = 0; b2 < KB; ++b2) {
-                            const double* pr = Lp + ((k + b2) * (k + b2 + 1)) / 2;
-                            p0[b2] = (b2 < kb) ? pr[j] : 0.0;
-                            p1[b2] = (b2 < kb && in1) ? pr[j + 1] : 0.0;
+                            p0[b2] = prb[b2][j];
+                            p1[b2] = prb[b2][j + 1];
                         }
                         const double s0 = (j < kf) ? -1.0 : 1.0, s1 = (j + 1 < kf) ? -1.0 : 1.0;
 #pragma unroll
