@@ -1647,9 +1647,15 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
             const int jm = j >> 1;
             int nnz = 0, jj = -1;
             // fixed trip count; gt(j, c) for c > j/2 still reads inside Gt (see check)
-            for (int c = 0; c < N; ++c) {
-                const double g = w.gt(j, c);
-                if (c <= jm && g != 0.0) { ++nnz; jj = c; }
+            constexpr int CH = 4;
+            for (int c0 = 0; c0 < N; c0 += CH) {          // batched loads
+                double g[CH];
+#pragma unroll
+                for (int u = 0; u < CH; ++u) g[u] = (c0 + u < N) ? w.gt(j, c0 + u) : 0.0;
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < CH; ++u)
+                    if (c0 + u <= jm && g[u] != 0.0) { ++nnz; jj = c0 + u; }
             }
             if (nnz == 1) {
                 double lv = sg * w.gt(j, jj);
@@ -1874,10 +1880,21 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
             // right-hand-side row holds sigma_k z_k (sigma = +1 free, -1 general
             // columns), which is exactly diag(I, -I) z
             double acc = (l < nt) ? Lp[(nt * (nt + 1)) / 2 + l] : 0.0, x = 0.0;
+            // the loads of column k-1 are issued before the broadcast of x_k (one-deep pipeline)
+            double lkn = 0.0, dkn = 0.0;
+            if (nt > 0) {
+                lkn = (l < nt - 1) ? Lp[((nt - 1) * nt) / 2 + l] : 0.0;
+                dkn = w.ldi()[nt - 1];
+            }
             for (int k = nt - 1; k >= 0; --k) {
-                const double xk = gbcast<P>(acc, k) * w.ldi()[k];
+                const double lk = lkn, dk = dkn;
+                if (k > 0) {
+                    lkn = (l < k - 1) ? Lp[((k - 1) * k) / 2 + l] : 0.0;
+                    dkn = w.ldi()[k - 1];
+                }
+                const double xk = gbcast<P>(acc, k) * dk;
                 if (l == k) x = xk;
-                if (l < k) acc -= Lp[(k * (k + 1)) / 2 + l] * xk;
+                if (l < k) acc -= lk * xk;
             }
             if (l >= nF && l < nt) w.np()[l - nF] = -x;
             NTM_WSYNC();
