@@ -1,12 +1,13 @@
 """Diagnostic (not a test): per-phase cycle breakdown of the fused step kernel
 using the -DNTM_STAMPS build (lib/libntm_mpc_diag.so)."""
 import ctypes as C, os, sys, time
-os.environ["NTM_MPC_LIB"] = os.path.join(os.path.dirname(__file__), "..", "mpc-ntm-control_amd", "lib", "libntm_mpc_diag.so")
+os.environ.setdefault("NTM_MPC_LIB", os.path.join(os.path.dirname(__file__), "..", "mpc-ntm-control_amd", "lib", "libntm_mpc_diag.so"))
 sys.path[:0] = [os.path.join(os.path.dirname(__file__), ".."), os.path.join(os.path.dirname(__file__), "..", "mpc-ntm-control_amd")]
 import torch, ntm_mpc
 from ntm_mpc import NtmMpc, Config
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 20000
-cfg = Config(N=20, mode=2)
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+cfg = Config(N=N, mode=int(sys.argv[3]) if len(sys.argv) > 3 else 2)
 ctl = NtmMpc(config=cfg)
 lib = ntm_mpc.load()
 buf = (C.c_ulonglong * 48)()
