@@ -1727,10 +1727,12 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
     // bordered rows do not fit the group's lanes or the block.
     const int nt = nF + nS;
     // nt <= 2N (nS <= nF); a compile-time horizon whose worst case fits compiles the fused path only
+    // Lanes own RPL bordered rows each (row l + r P), enough for the nt + 1 <= 2N + 1 rows
     constexpr int NNc = W::kNN, LDc = NNc | 1;
+    constexpr int RPL = NNc > 0 ? (2 * NNc + 1 + P - 1) / P : (2 * NTM_MAX_N + 1 + P - 1) / P;
     constexpr bool kAlwaysFused =
-        NNc > 0 && 2 * NNc + 1 <= P && (2 * NNc) * (2 * NNc + 1) / 2 + 2 * NNc <= NNc * LDc + (NNc + 1) * LDc;
-    const bool fused = kAlwaysFused || ((nt + 1 <= P) && (nt * (nt + 1) / 2 + nt <= N * LDJ + (N + 1) * LD));
+        NNc > 0 && (2 * NNc) * (2 * NNc + 1) / 2 + 2 * NNc <= NNc * LDc + (NNc + 1) * LDc;
+    const bool fused = kAlwaysFused || ((nt + 1 <= RPL * P) && (nt * (nt + 1) / 2 + nt <= N * LDJ + (N + 1) * LD));
     double* const Lp = w.J();
     if (fused && l < nF) Lp[(nt * (nt + 1)) / 2 + l] = -gl;
     // --- compact G~_FF: one (a, c) entry per lane (packed rows, or lower col-major in R) ---
@@ -1802,35 +1804,56 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
         // Y = L^{-1} E', L_K L_K' = K = Y'Y (the Schur complement), in one pass
         // whose right-hand-side row carries the forward substitution
         // z = L_A^{-1} [-g_F; h].  Lane r owns row r.
-        double* const myrow = Lp + (l * (l + 1)) / 2;
+        // Lane l owns rows l + r P (r < RPL); a group-uniform row index k lives on
+        // lane k % P in slot k / P.
+        auto slot_of = [&](const double* v, int k) -> double {   // v[k / P] (k uniform)
+            double o = v[0];
+#pragma unroll
+            for (int r = 1; r < RPL; ++r) o = (k / P == r) ? v[r] : o;
+            return o;
+        };
+        double* myrow[RPL];
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+            const int lr = l + r * P;
+            myrow[r] = Lp + (lr * (lr + 1)) / 2;
+        }
         if (ok) {
             // blocks of KB columns: one pass of loads over the finished columns j < k
             // serves all KB pivot rows, then the block's own triangle is finished in
-            // registers (L[k+b, k+c] broadcast from lane k+b).  Each column still
-            // accumulates its terms in column order, as the unblocked elimination.
+            // registers (L[k+b, k+c] broadcast from the lane of row k+b).  Each column
+            // still accumulates its terms in column order, as the unblocked elimination.
             constexpr int KB = 4;
             for (int k = 0; k < nt; k += KB) {
                 const int kb = (nt - k < KB) ? nt - k : KB;
-                const bool live = l >= k && l <= nt;
-                double sacc[KB];
+                double sacc[RPL][KB];
+                bool live[RPL];
 #pragma unroll
-                for (int b2 = 0; b2 < KB; ++b2) {
-                    const int col = k + b2;
-                    sacc[b2] = (b2 < kb && live && l >= col) ? ((col >= nF && l < nt) ? 0.0 : myrow[col]) : 0.0;
-                }
-                if (live) {
-                    const int kf = k < nF ? k : nF;
-                    // unconditional loads (no branch per load): j + 1 <= k stays inside row l
-                    // (l >= k) and row k+b2; pivot rows past the block clamp to row nt
-                    const double* prb[KB];
+                for (int r = 0; r < RPL; ++r) {
+                    const int lr = l + r * P;
+                    live[r] = lr >= k && lr <= nt;
 #pragma unroll
                     for (int b2 = 0; b2 < KB; ++b2) {
-                        const int rr = (k + b2 < nt) ? k + b2 : nt;
-                        prb[b2] = Lp + (rr * (rr + 1)) / 2;
+                        const int col = k + b2;
+                        sacc[r][b2] = (b2 < kb && live[r] && lr >= col) ? ((col >= nF && lr < nt) ? 0.0 : myrow[r][col])
+                                                                        : 0.0;
                     }
+                }
+                const int kf = k < nF ? k : nF;
+                // unconditional loads (no branch per load): j + 1 <= k stays inside each
+                // live row (>= k) and pivot row k+b2; pivot rows past the block clamp to row nt
+                const double* prb[KB];
+#pragma unroll
+                for (int b2 = 0; b2 < KB; ++b2) {
+                    const int rr = (k + b2 < nt) ? k + b2 : nt;
+                    prb[b2] = Lp + (rr * (rr + 1)) / 2;
+                }
+#pragma unroll
+                for (int r = 0; r < RPL; ++r) {
+                    if (!live[r]) continue;
                     for (int j = 0; j < k; j += 2) {
                         const bool in1 = j + 1 < k;
-                        const double a0 = myrow[j], a1 = myrow[j + 1];
+                        const double a0 = myrow[r][j], a1 = myrow[r][j + 1];
                         double p0[KB], p1[KB];
 #pragma unroll
                         for (int b2 = 0; b2 < KB; ++b2) {
@@ -1840,37 +1863,52 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
                         const double s0 = (j < kf) ? -1.0 : 1.0, s1 = (j + 1 < kf) ? -1.0 : 1.0;
 #pragma unroll
                         for (int b2 = 0; b2 < KB; ++b2) {
-                            sacc[b2] += (s0 * a0) * p0[b2];
-                            sacc[b2] += in1 ? (s1 * a1) * p1[b2] : 0.0;
+                            sacc[r][b2] += (s0 * a0) * p0[b2];
+                            sacc[r][b2] += in1 ? (s1 * a1) * p1[b2] : 0.0;
                         }
                     }
                 }
-                double Lc[KB];
+                double Lc[RPL][KB];
 #pragma unroll
                 for (int b2 = 0; b2 < KB; ++b2) {
-                    Lc[b2] = 0.0;
+#pragma unroll
+                    for (int r = 0; r < RPL; ++r) Lc[r][b2] = 0.0;
                     if (b2 < kb) {
-                        const int col = k + b2;
+                        const int col = k + b2, cl = col % P;
 #pragma unroll
                         for (int c = 0; c < b2; ++c) {           // block columns k..col-1, in order
-                            const double lkc = gbcast<P>(Lc[c], col);   // L[col, k+c] from lane col
+                            double lcc[RPL];
+#pragma unroll
+                            for (int r = 0; r < RPL; ++r) lcc[r] = Lc[r][c];
+                            const double lkc = gbcast<P>(slot_of(lcc, col), cl);   // L[col, k+c]
                             const double sc = (k + c < nF) ? -1.0 : 1.0;
-                            sacc[b2] += (sc * Lc[c]) * lkc;
+#pragma unroll
+                            for (int r = 0; r < RPL; ++r) sacc[r][b2] += (sc * Lc[r][c]) * lkc;
                         }
-                        const double sk = (col < nF) ? sacc[b2] : -sacc[b2];
-                        const double dk = gbcast<P>(sk, col);
+                        double skr[RPL];
+#pragma unroll
+                        for (int r = 0; r < RPL; ++r) skr[r] = (col < nF) ? sacc[r][b2] : -sacc[r][b2];
+                        const double dk = gbcast<P>(slot_of(skr, col), cl);
                         if (!(dk > 0.0) || !(dk < kInf)) { ok = false; fk = 3; }
                         else {
                             const double il = rsqrt_nr(dk);
-                            Lc[b2] = (l == col) ? dk * il : sk * il;
-                            if (l == col) w.ldi()[col] = il;          // ldi/kdi: 2N contiguous
+#pragma unroll
+                            for (int r = 0; r < RPL; ++r) {
+                                const int lr = l + r * P;
+                                Lc[r][b2] = (lr == col) ? dk * il : skr[r] * il;
+                                if (lr == col) w.ldi()[col] = il;   // ldi/kdi: 2N contiguous
+                            }
                         }
                     }
                 }
                 if (!ok) break;
 #pragma unroll
-                for (int b2 = 0; b2 < KB; ++b2)
-                    if (b2 < kb && l >= k + b2 && l <= nt) myrow[k + b2] = Lc[b2];
+                for (int r = 0; r < RPL; ++r) {
+                    const int lr = l + r * P;
+#pragma unroll
+                    for (int b2 = 0; b2 < KB; ++b2)
+                        if (b2 < kb && lr >= k + b2 && lr <= nt) myrow[r][k + b2] = Lc[r][b2];
+                }
                 NTM_WSYNC();
             }
         }
@@ -1879,26 +1917,50 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
             // L_A' x = diag(I, -I) z: x = [V_F; -mu], one backward sweep.  The
             // right-hand-side row holds sigma_k z_k (sigma = +1 free, -1 general
             // columns), which is exactly diag(I, -I) z
-            double acc = (l < nt) ? Lp[(nt * (nt + 1)) / 2 + l] : 0.0, x = 0.0;
-            // the loads of column k-1 are issued before the broadcast of x_k (one-deep pipeline)
-            double lkn = 0.0, dkn = 0.0;
-            if (nt > 0) {
-                lkn = (l < nt - 1) ? Lp[((nt - 1) * nt) / 2 + l] : 0.0;
-                dkn = w.ldi()[nt - 1];
+            double acc[RPL], x[RPL];
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) {
+                const int lr = l + r * P;
+                acc[r] = (lr < nt) ? Lp[(nt * (nt + 1)) / 2 + lr] : 0.0;
+                x[r] = 0.0;
             }
+            // the loads of column k-1 are issued before the broadcast of x_k (one-deep pipeline)
+            double lkn[RPL], dkn = 0.0;
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) {
+                const int lr = l + r * P;
+                lkn[r] = (nt > 0 && lr < nt - 1) ? Lp[((nt - 1) * nt) / 2 + lr] : 0.0;
+            }
+            if (nt > 0) dkn = w.ldi()[nt - 1];
             for (int k = nt - 1; k >= 0; --k) {
-                const double lk = lkn, dk = dkn;
+                double lk[RPL];
+#pragma unroll
+                for (int r = 0; r < RPL; ++r) lk[r] = lkn[r];
+                const double dk = dkn;
                 if (k > 0) {
-                    lkn = (l < k - 1) ? Lp[((k - 1) * k) / 2 + l] : 0.0;
+#pragma unroll
+                    for (int r = 0; r < RPL; ++r) {
+                        const int lr = l + r * P;
+                        lkn[r] = (lr < k - 1) ? Lp[((k - 1) * k) / 2 + lr] : 0.0;
+                    }
                     dkn = w.ldi()[k - 1];
                 }
-                const double xk = gbcast<P>(acc, k) * dk;
-                if (l == k) x = xk;
-                if (l < k) acc -= lk * xk;
+                const double xk = gbcast<P>(slot_of(acc, k), k % P) * dk;
+#pragma unroll
+                for (int r = 0; r < RPL; ++r) {
+                    const int lr = l + r * P;
+                    if (lr == k) x[r] = xk;
+                    if (lr < k) acc[r] -= lk[r] * xk;
+                }
             }
-            if (l >= nF && l < nt) w.np()[l - nF] = -x;
+#pragma unroll
+            for (int r = 0; r < RPL; ++r) {
+                const int lr = l + r * P;
+                if (lr >= nF && lr < nt) w.np()[lr - nF] = -x[r];
+            }
             NTM_WSYNC();
-            const double vsc = __shfl(x, (l < N && !fixed) ? fpos : 0, P);
+            // V_F sits in rows < nF <= N <= P: slot 0
+            const double vsc = __shfl(x[0], (l < N && !fixed) ? fpos : 0, P);
             vfin = fixed ? vb : vsc;
         }
         NTM_ACC(ST_S_SOLVE, tp);
