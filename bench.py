@@ -38,8 +38,8 @@ HBM_PEAK_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=100_000, help="scenarios per GPU")
     ap.add_argument("--N", type=int, default=20)
     ap.add_argument("--mode", type=int, default=2)
@@ -201,14 +201,16 @@ def main():
     flop_step = FL.per_step(N, args.mode, qps, tries, giruns, Kgi, qact, sgen)
     achieved = flop_step * B / (kern_ms * 1e-3) / 1e12
     traffic = None
-    prof = ROOT / "profiles" / "traffic_r01.json"
-    if prof.exists():
+    # PMC-measured HBM bytes per launch of this workload (tools/traffic_run.py,
+    # separate FETCH_SIZE / WRITE_SIZE passes): the latest round's file that matches
+    for prof in sorted((ROOT / "profiles").glob("traffic_r*.json"), reverse=True):
         try:
             tj = json.loads(prof.read_text())
-            if tj.get("B") == B and tj.get("N") == N:
-                traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
-            traffic = None
+            continue
+        if tj.get("B") == B and tj.get("N") == N and tj.get("mode", 2) == args.mode:
+            traffic = tj.get("hbm_bytes_per_launch")
+            break
     res = {
         "metric": "MPC steps/sec (whole node) at horizon N=20, batch=1e5 scenarios",
         "value": value,
@@ -227,12 +229,13 @@ def main():
                    "scenarios_per_gpu": B, "global_batch": world * B, "N": N, "mode": args.mode, "i_sim": 10,
                    "parallelism": f"scenario-sharded x{world} (weak), end-of-batch all_gather"
                        + (" [gloo rehearsal: ranks share devices]" if rehearsal and world > 1 else "")},
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "roofline": {"bound": "valu-fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": ctl.step_kernel_name(B, cfg), "kernel_avg_ms": kern_ms,
                      "flop_per_step": flop_step,
                      "hbm_algorithmic_bytes_per_launch": FL.hbm_bytes_per_step(N, workspace=True) * B,
-                     "note": "fp64 VALU work; peak = MI355X dense fp64 (vector == matrix rate)"},
+                     "note": "fp64 VALU work (DPP/LDS, no MFMA: DESIGN.md §6); peak = MI355X fp64 vector rate "
+                             "(78.6 TF, equal to the fp64 matrix rate)"},
         "solver": {"inner_iters_mean": iters, "qp_per_step": qps, "warm_verify_per_step": tries,
                    "gi_solves_per_step": giruns, "gi_iters_per_step": Kgi,
                    "active_rows_per_qp": qact, "state_rows_per_qp": sgen, "optimal_frac": n_opt / B},

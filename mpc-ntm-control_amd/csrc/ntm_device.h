@@ -367,10 +367,15 @@ __host__ __device__ inline int ldj_of(int N) { return N | 1; }
 __host__ __device__ inline int ws_doubles(int N) {
     return 14 * N + N * (N + 1) + (N <= kMaxNT ? 2 : 1) * N * ldj_of(N) + (N + 1) * ldj_of(N) + 24 * N + 3;
 }
-__host__ __device__ inline int ws_bytes(int N) {
-    int b = ws_doubles(N) * 8 + 6 * (N + 1) * 4 + N + (8 * N + 4);   // ..., fx (N), aflag (rows <= 8N+2)
+// workspace bytes with room for `rows` active-row flags: the structured rows of
+// the MPC step are at most 8N+2 (getWLc 6N+4 plus 2(N-1) rate rows); a dense
+// quadprog problem (k_qp) may carry more
+__host__ __device__ inline int ws_bytes_rows(int N, int rows) {
+    const int flags = rows > 8 * N + 4 ? rows : 8 * N + 4;
+    int b = ws_doubles(N) * 8 + 6 * (N + 1) * 4 + N + flags;   // ..., fx (N), aflag
     return (b + 15) & ~15;
 }
+__host__ __device__ inline int ws_bytes(int N) { return ws_bytes_rows(N, 8 * N + 4); }
 
 template <int NN>
 __device__ inline WS<NN> ws_carve(char* base, int N) {
@@ -2112,20 +2117,20 @@ __device__ bool rollout_phase(const Prob& pb, const W& w, double x0, double x1, 
         }
     }
     NTM_WSYNC();
-    double dsum = 0.0;
+    double dsum = 0.0, u = 0.0;
     if (l < N) {
         double r1, r2, r3;
         rho_eval(k, w.xp()[2 * l], w.xp()[2 * l + 1], r1, r2, r3);
         w.rho()[3 * l] = r1;
         w.rho()[3 * l + 1] = r2;
         w.rho()[3 * l + 2] = r3;
-        double u = w.U()[l];
+        u = w.U()[l];
         dsum = fabs(w.Uold()[l] - u);
-        w.Uold()[l] = u;
     }
+    const bool conv = gsum<P>(dsum) < pb.eps;      // :123
+    if (!conv && l < N) w.Uold()[l] = u;           // :127; the break at :125 skips it
     NTM_WSYNC();
-    double s = gsum<P>(dsum);
-    return s < pb.eps;
+    return conv;
 }
 
 // plant step NTM_MPC_Sim.m:130 (CANON D13: plant = prediction model, + C)

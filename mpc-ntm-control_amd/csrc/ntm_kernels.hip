@@ -381,10 +381,11 @@ __global__ __launch_bounds__(64) void k_qp(int64_t B, int N, int m, const double
     const int g = threadIdx.x / P, l = threadIdx.x % P;
     const int64_t s = (int64_t)blockIdx.x * G + g;
     if (s >= B) return;
-    const int wsb = ws_bytes(N) + ((m * 8 + 15) & ~15) + N * ldj_of(N) * 8;
+    const int wsm = ws_bytes_rows(N, m);        // active-row flags sized for all m rows
+    const int wsb = wsm + ((m * 8 + 15) & ~15) + N * ldj_of(N) * 8;
     char* base = smem + g * wsb;
     auto w = ws_carve<NN>(base, N);
-    double* rnrm = reinterpret_cast<double*>(base + ws_bytes(N));
+    double* rnrm = reinterpret_cast<double*>(base + wsm);
     double* gsave = rnrm + ((m + 1) & ~1);     // copy of G~ for the polish (N x LDJ)
     if (l < N) {
         for (int kk = 0; kk <= l; ++kk) w.R()[l + kk * w.ldj()] = G_in[s * (N * N) + l + kk * N];
@@ -484,6 +485,23 @@ struct ntm_ctx {
 };
 
 namespace {
+
+// Makes ctx->device current for the duration of an entry point and restores the
+// caller's device on exit: hipMalloc, hipFuncSetAttribute (the > 64 KiB LDS
+// opt-in) and the launches all act on the current device.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(const ntm_ctx* ctx) {
+        int cur = -1;
+        if (ctx && hipGetDevice(&cur) == hipSuccess && cur != ctx->device && hipSetDevice(ctx->device) == hipSuccess)
+            prev = cur;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
 
 int fail(ntm_ctx* ctx, int code, const std::string& msg) {
     if (ctx) ctx->err = msg;
@@ -648,6 +666,7 @@ int ntm_ctx_create(ntm_ctx** out, int32_t device) {
 
 void ntm_ctx_destroy(ntm_ctx* ctx) {
     if (!ctx) return;
+    DeviceGuard dg(ctx);
     if (ctx->dbuf) (void)hipFree(ctx->dbuf);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -689,6 +708,7 @@ int ntm_mpc_step_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config*
 int ntm_mpc_step_ws_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B,
                            const double* x_k, double* rho, double* U_old, double* U, double* x_pred, double* x_next,
                            int32_t* exitflag, int32_t* inner_iters, int32_t* active_ws, void* stream) {
+    DeviceGuard dg(ctx);
     int rc = validate(ctx, phys, cfg, B);
     if (rc) return rc;
     if (B == 0) return NTM_OK;
@@ -719,6 +739,7 @@ int ntm_mpc_step(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, i
 int ntm_mpc_step_ws(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* x_k,
                     double* rho, double* U_old, double* U, double* x_pred, double* x_next, int32_t* exitflag,
                     int32_t* inner_iters, int32_t* active_ws) {
+    DeviceGuard dg(ctx);
     int rc = validate(ctx, phys, cfg, B);
     if (rc) return rc;
     if (B == 0) return NTM_OK;
@@ -764,6 +785,7 @@ int ntm_mpc_step_ws(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg
 int ntm_mpc_run_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, int32_t k_sim,
                        const double* x0, double* xk, double* uk, double* Uk, double* wpred, int32_t* exitflag,
                        int32_t* inner_iters, void* stream) {
+    DeviceGuard dg(ctx);
     int rc = validate(ctx, phys, cfg, B);
     if (rc) return rc;
     if (k_sim < 0) return fail(ctx, NTM_E_INVALID, "negative k_sim");
@@ -780,6 +802,7 @@ int ntm_mpc_run_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* 
 int ntm_mpc_run(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, int32_t k_sim,
                 const double* x0, double* xk, double* uk, double* Uk, double* wpred, int32_t* exitflag,
                 int32_t* inner_iters) {
+    DeviceGuard dg(ctx);
     int rc = validate(ctx, phys, cfg, B);
     if (rc) return rc;
     if (k_sim < 0) return fail(ctx, NTM_E_INVALID, "negative k_sim");
@@ -816,6 +839,7 @@ int ntm_mpc_run(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, in
 
 int ntm_rho_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* x,
                    double* rho, void* stream) {
+    DeviceGuard dg(ctx);
     int rc = validate(ctx, phys, cfg, B);
     if (rc || B == 0) return rc;
     Prob pb = make_prob(phys, cfg);
@@ -825,6 +849,7 @@ int ntm_rho_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg,
 
 int ntm_mpc_init_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* x0,
                         double* rho, double* U_old, void* stream) {
+    DeviceGuard dg(ctx);
     int rc = validate(ctx, phys, cfg, B);
     if (rc || B == 0) return rc;
     if (!x0 || !rho || !U_old) return fail(ctx, NTM_E_INVALID, "null array");
@@ -836,6 +861,7 @@ int ntm_mpc_init_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config*
 
 int ntm_mpc_init(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* x0,
                  double* rho, double* U_old) {
+    DeviceGuard dg(ctx);
     int rc = validate(ctx, phys, cfg, B);
     if (rc || B == 0) return rc;
     if (!x0 || !rho || !U_old) return fail(ctx, NTM_E_INVALID, "null array");
@@ -856,6 +882,7 @@ int ntm_mpc_init(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, i
 
 int ntm_AB_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* rho,
                   double* A, double* Bv, void* stream) {
+    DeviceGuard dg(ctx);
     int rc = validate(ctx, phys, cfg, B);
     if (rc || B == 0) return rc;
     Prob pb = make_prob(phys, cfg);
@@ -884,6 +911,7 @@ int ntm_AB_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, 
 
 int ntm_lift_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* rho,
                     double* Phi, double* Gamma, double* Lambda, void* stream) {
+    DeviceGuard dg(ctx);
     int rc = validate(ctx, phys, cfg, B);
     if (rc || B == 0) return rc;
     Prob pb = make_prob(phys, cfg);
@@ -893,6 +921,7 @@ int ntm_lift_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg
 
 int ntm_cost_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* rho,
                     const double* x_k, double* G, double* F, void* stream) {
+    DeviceGuard dg(ctx);
     int rc = validate(ctx, phys, cfg, B);
     if (rc || B == 0) return rc;
     Prob pb = make_prob(phys, cfg);
@@ -902,6 +931,7 @@ int ntm_cost_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg
 
 int ntm_getwlc_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B, const double* rho,
                       double* W, double* L, double* c, void* stream) {
+    DeviceGuard dg(ctx);
     int rc = validate(ctx, phys, cfg, B);
     if (rc || B == 0) return rc;
     Prob pb = make_prob(phys, cfg);
@@ -911,13 +941,16 @@ int ntm_getwlc_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* c
 
 int ntm_qp_device(ntm_ctx* ctx, int64_t B, int32_t N, int32_t m, const double* G, const double* F,
                   const double* Lin, const double* b, double* U, int32_t* exitflag, int32_t* iters, void* stream) {
+    DeviceGuard dg(ctx);
     if (!ctx) return NTM_E_INVALID;
     if (N < 1 || N > NTM_MAX_N) return fail(ctx, NTM_E_INVALID, "N out of range [1, 64]");
     if (m < 0 || m > 6 * NTM_MAX_N + 4) return fail(ctx, NTM_E_INVALID, "m out of range");
     if (B < 0) return fail(ctx, NTM_E_INVALID, "negative batch");
     if (B == 0) return NTM_OK;
+    if (!G || !F || !U || !exitflag) return fail(ctx, NTM_E_INVALID, "null array");
+    if (m > 0 && (!Lin || !b)) return fail(ctx, NTM_E_INVALID, "m > 0 needs Lin and b");
     int P = lanes_for(N), Gs = 64 / P;
-    size_t per = (size_t)ws_bytes(N) + ((m * 8 + 15) & ~15) + (size_t)N * ldj_of(N) * 8;
+    size_t per = (size_t)ws_bytes_rows(N, m) + ((m * 8 + 15) & ~15) + (size_t)N * ldj_of(N) * 8;
     size_t lds = Gs * per;
     unsigned blocks = (unsigned)((B + Gs - 1) / Gs);
     hipStream_t st = (hipStream_t)stream;

@@ -598,8 +598,8 @@ static void orc_step(const orc_coef* k, const ntm_config* c, const double* x,
         }
         double s = 0.0;                                      /* :123 */
         for (int j = 0; j < N; ++j) s += fabs(Uold[j] - U[j]);
-        for (int j = 0; j < N; ++j) Uold[j] = U[j];          /* :127 */
-        if (s < c->epsilon) break;
+        if (s < c->epsilon) break;                           /* :125, before :127 */
+        for (int j = 0; j < N; ++j) Uold[j] = U[j];          /* :127 (skipped on break) */
     }
     if (it > c->i_sim) it = c->i_sim;
     /* plant step (:130, D13) */

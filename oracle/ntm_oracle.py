@@ -674,10 +674,9 @@ def mpc_step(xk, Rho, Uold, phys: Physics, cfg: Config, polish=False):
         Lin, bvec = constraints(Phi, Gam, Lam, xk, cfg)
         U, flag, _ = qp_solve(G, F, Lin, bvec, polish=polish)
         xp, Rho = rollout(xk, Rho, U, phys, cfg)
-        conv = np.sum(np.abs(Uold - U)) < cfg.epsilon        # :123
-        Uold = U.copy()                                      # :127 (kept also on break)
-        if conv:
-            break
+        if np.sum(np.abs(Uold - U)) < cfg.epsilon:           # :123
+            break                                            # :125, before :127
+        Uold = U.copy()                                      # :127 (skipped on break)
     xn = plant_step(xk, U[0], phys, cfg)
     return {"U": U, "u": U[0], "xpred": xp, "xnext": xn, "Rho": Rho, "Uold": Uold,
             "exitflag": flag, "inner_iters": it}
