@@ -111,7 +111,7 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        ST_GI_DIR, ST_GI_ADD, ST_GI_DROP, CN_CHECK, CN_CAND, CN_HIT,
        ST_P_CLASS, ST_P_GRAM, ST_P_CHOL, ST_P_SCHUR, ST_P_BWD, ST_P_KKT, CN_REPAIR, CN_GIRUN,
        ST_S_E, ST_S_Y, ST_S_K, ST_S_CHOL, ST_S_SOLVE, CN_TRY_EARLY, CN_FAIL_EARLY, CN_FAIL_LATE,
-       CN_FAIL_IT1, CN_FAIL_IT2, CN_GI_IT1, CN_GI_IT2, CN_GI_LATE, CN_TRY_IT1, CN_TRY_IT2, CN_WARM_TRY, CN_WARM_OK, CN_WARM_DEP, CN_WARM_NEG, CN_WARM_FULL };
+       CN_FAIL_IT1, CN_FAIL_IT2, CN_GI_IT1, CN_GI_IT2, CN_GI_LATE, CN_TRY_IT1, CN_TRY_IT2, CN_WARM_TRY, CN_WARM_OK, CN_WARM_DEP, CN_WARM_NEG, CN_WARM_FULL, CN_ALT_TRY, CN_ALT_HIT };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 constexpr int kMaxNT = 32;         // explicit R^{-1} in GI up to this horizon (WS::useT)
 constexpr int kRepairs = 8;        // single-row repairs of a failed warm-start candidate
@@ -2073,7 +2073,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
         double mkey = has ? mval : kInf;
         gargmin<P>(mkey, mpos);
         const bool dual_ok = !(mkey < -1e-9 * fmax(1.0, mabs));
-        fk = !ok ? 2 : (!dual_ok ? 1 : 0);
+        fk = !ok ? (dual_ok ? 2 : 4) : (!dual_ok ? 1 : 0);
         fpos_out = mpos;
         ok = ok && dual_ok;
     }
@@ -2146,57 +2146,53 @@ __device__ __forceinline__ void plant_step(const Prob& pb, double x0, double x1,
 }
 
 // ---------------------------------------------------------------------------
-// Receding-horizon shift of the carried warm-start set tried at inner
-// iteration 2 (start of an MPC step).  The previous step planned stages
-// k..k+N-1; this step plans k+1..k+N, so a row of stage i >= 1 moves to stage
-// i-1, stage-0 rows are dropped, and the bound rows of the old last input are
-// kept for the new last input as well.  Iteration 1 keeps its set unshifted:
-// its QP still runs on the previous step's (unshifted, D20) scheduling
-// parameters, and measured on MI355X (B=1e5, N=20) shifting that set doubles
-// its GI fallbacks, while shifting the iteration-2 set cuts them by a third.
-// Only a hint: every candidate is re-solved exactly and KKT-certified.
+// Receding-horizon shift of a carried warm-start set, into w.act() (returns
+// the shifted count).  The previous step planned stages k..k+N-1; this step
+// plans k+1..k+N, so a row of stage i >= 1 moves to stage i-1, stage-0 rows
+// are dropped, and the bound rows of the old last input and the terminal state
+// rows are kept for the new last stage as well.  It is the SECOND candidate of inner iteration 2, after
+// the unshifted set: in the closed loop's steady state the LPV iteration
+// 2-cycles through the same pair of active sets every step (the odd and even
+// iterations), so the previous step's set hits unshifted (70% at iteration 2
+// over steps 5-20, against 7% shifted; 36% vs 31% over steps 1-4, where the
+// plan still moves in time).  Only a hint: every candidate is re-solved
+// exactly and KKT-certified.
 // ---------------------------------------------------------------------------
 template <int P, class W>
-__device__ void shift_candidates(const Prob& pb, const W& w, int l) {
+__device__ int shifted_into_act(const Prob& pb, const W& w, const int* c, int l) {
     const int N = w.n();
-    if (pb.mode == NTM_MODE_NONE) return;
     const int lane = threadIdx.x & 63;
     const unsigned long long gmask = (P == 64) ? ~0ull : (((1ull << P) - 1ull) << (lane & ~(P - 1)));
     const unsigned long long below = (1ull << lane) - 1ull;
-    {
-        int* c = w.cand() + (N + 1);                           // slot 1: tried at iteration 2
-        const int q = uni<P>(c[N]);
-        if (q <= 0) return;
-        int nid = -1, dup = -1;
-        if (l < q) {
-            const int id = c[l];
-            if (pb.mode == NTM_MODE_BOX) {
-                const int j = id < N ? id : id - N;
-                if (j >= 1) nid = id - 1;
-                if (j == N - 1) dup = id;
-            } else if (id >= 6 * N + 4) {                    // rate row of input j
-                const int j = ((id - (6 * N + 4)) >> 1) + 1;
-                if (j >= 2) nid = id - 2;
-                if (j == N - 1) dup = id;
-            } else if (id >= 6 * N) {                        // terminal state row -> stage N-1
-                nid = 6 * (N - 1) + 2 + (id - 6 * N);
-            } else {
-                const int blk = id / 6, rr = id - 6 * blk;
-                if (blk >= 1) nid = id - 6;
-                if (blk == N - 1 && rr < 2) dup = id;
-            }
+    const int q = uni<P>(c[N]);
+    int nid = -1, dup = -1;
+    if (l < q) {
+        const int id = c[l];
+        if (pb.mode == NTM_MODE_BOX) {
+            const int j = id < N ? id : id - N;
+            if (j >= 1) nid = id - 1;
+            if (j == N - 1) dup = id;
+        } else if (id >= 6 * N + 4) {                    // rate row of input j
+            const int j = ((id - (6 * N + 4)) >> 1) + 1;
+            if (j >= 2) nid = id - 2;
+            if (j == N - 1) dup = id;
+        } else if (id >= 6 * N) {                        // terminal state row -> stage N-1, and kept
+            nid = 6 * (N - 1) + 2 + (id - 6 * N);
+            dup = id;
+        } else {
+            const int blk = id / 6, rr = id - 6 * blk;
+            if (blk >= 1) nid = id - 6;
+            if (blk == N - 1 && rr < 2) dup = id;
         }
-        NTM_WSYNC();
-        const unsigned long long bk = __ballot(nid >= 0) & gmask;
-        const unsigned long long bd = __ballot(dup >= 0) & gmask;
-        const int nk = uni<P>((int)__popcll(bk)), nd = uni<P>((int)__popcll(bd));
-        const bool with_dup = nk + nd <= N;
-        if (nid >= 0) c[__popcll(bk & below)] = nid;
-        if (with_dup && dup >= 0) c[nk + __popcll(bd & below)] = dup;
-        NTM_WSYNC();
-        if (l == 0) c[N] = nk + (with_dup ? nd : 0);
-        NTM_WSYNC();
     }
+    const unsigned long long bk = __ballot(nid >= 0) & gmask;
+    const unsigned long long bd = __ballot(dup >= 0) & gmask;
+    const int nk = uni<P>((int)__popcll(bk)), nd = uni<P>((int)__popcll(bd));
+    const bool with_dup = nk + nd <= N;
+    if (nid >= 0) w.act()[__popcll(bk & below)] = nid;
+    if (with_dup && dup >= 0) w.act()[nk + __popcll(bd & below)] = dup;
+    NTM_WSYNC();
+    return nk + (with_dup ? nd : 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -2216,7 +2212,7 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
     int flag, q = 0, ns = 0;
     *qp_iters = 0;
     StructRows rows(pb);
-    int* cand = w.cand() + slot * (N + 1);
+    int* cand = w.cand() + slot * (N + 1);               // this QP's active set is stored here
     if (!diag_scale_phase<P>(pb, w, l, full)) {
         flag = NTM_EXIT_NONFINITE;
     } else {
@@ -2241,8 +2237,14 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                 int cq = cq0;
                 if (l < cq) w.act()[l] = cand[l];
                 NTM_WSYNC();
+                // iteration 2: the carried set is the previous step's (slot 1 is only
+                // written at even iterations); when its repairs fail, its
+                // receding-horizon shift is tried before GI (it hits in the
+                // transient of the first steps, where the plan moves in time)
+                bool alt = it == 2 && pb.mode != NTM_MODE_NONE;
+                int keep_id = -1, keep_q = -1;     // the repaired set (lane l: entry l) while the shift is tried
                 // certified re-solve of the candidate; on failure, up to kRepairs
-                // single-row repairs (add the most violated row, or drop the row
+                // single-row repairs (add the most violated row and/or drop the row
                 // with the most negative multiplier) before falling back to GI.
                 // Only a set that passes the KKT certificate is ever accepted.
                 for (int rep = 0;; ++rep) {
@@ -2257,6 +2259,7 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                         if (it == 1) { NTM_CNT(CN_TRY_IT1); if (!okc) NTM_CNT(CN_FAIL_IT1); }
                         if (it == 2) { NTM_CNT(CN_TRY_IT2); if (!okc) NTM_CNT(CN_FAIL_IT2); }
                     }
+                    if (rep < 0 && okc) NTM_CNT(CN_ALT_HIT);
                     if (okc) {
                         flag = NTM_EXIT_OPTIMAL;
                         q = cq;
@@ -2265,8 +2268,8 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                         if (rep > 0) NTM_CNT(CN_REPAIR);
                         break;
                     }
-                    if (rep == kRepairs || fk == 3) break;
-                    if (fk == 2) {                         // primal: add the most violated row
+                    bool stop = rep >= kRepairs || rep < 0 || fk == 3;   // rep < 0: the shifted set failed
+                    if (!stop && (fk == 2 || fk == 4)) {   // primal: add the most violated row
                         if (l < cq) w.aflag()[w.act()[l]] = kActiveRow;
                         NTM_WSYNC();
                         const double vmx = gmax<P>(l < N ? fabs(vf) : 0.0);
@@ -2274,23 +2277,39 @@ __device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l,
                         NTM_WSYNC();
                         if (l < cq) w.aflag()[w.act()[l]] = 0;
                         NTM_WSYNC();
-                        if (pk.p < 0) break;
-                        if (cq < N) {
+                        if (pk.p < 0) {
+                            stop = true;
+                        } else if (cq < N && fk == 2) {
                             if (l == 0) w.act()[cq] = pk.p;
                             ++cq;
-                        } else if (l == 0) {               // full set: swap out the smallest multiplier
-                            w.act()[fp] = pk.p;
+                        } else if (l == 0) {               // a negative multiplier too (fk 4), or a full
+                            w.act()[fp] = pk.p;            // set: it swaps out the smallest multiplier
                         }
-                    } else {                               // dual: drop position fp
+                    } else if (!stop) {                    // dual: drop position fp
                         int an = 0;
                         if (l >= fp && l + 1 < cq) an = w.act()[l + 1];
                         NTM_WSYNC();
                         if (l >= fp && l + 1 < cq) w.act()[l] = an;
                         --cq;
                     }
+                    if (stop) {
+                        if (!alt) break;
+                        alt = false;                       // last try: the shifted carried set
+                        NTM_CNT(CN_ALT_TRY);
+                        keep_id = (l < cq) ? w.act()[l] : -1;
+                        keep_q = cq;
+                        NTM_WSYNC();
+                        cq = shifted_into_act<P>(pb, w, cand, l);
+                        rep = -2;                          // counted as neither a first try nor a repair
+                    }
                     NTM_WSYNC();
                 }
                 if (!done) {
+                    if (keep_q >= 0) {                     // back to the repaired set
+                        cq = keep_q;
+                        if (l < cq) w.act()[l] = keep_id;
+                        NTM_WSYNC();
+                    }
                     // the repaired set steers GI's add order (StructRows::check) and,
                     // is GI's warm-start set (gi_solve)
                     if (l < cq) {

@@ -153,7 +153,6 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, 
     const double x0 = x_k[2 * s], x1 = x_k[2 * s + 1];
     if (active_ws) {
         load_candidates<P>(pb, w, B, s, active_ws, l);
-        shift_candidates<P>(pb, w, l);
     } else if (l < 2) {
         w.cand()[l * (N + 1) + N] = -1;
     }
@@ -209,7 +208,6 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_run(Prob pb, i
     }
     if (xk && l == 0) { xk[s * 2 * (k_sim + 1)] = x0; xk[s * 2 * (k_sim + 1) + 1] = x1; }
     for (int kk = 0; kk < k_sim; ++kk) {
-        if (kk > 0) shift_candidates<P>(pb, w, l);
         int its;
         int flag = mpc_step_dev<P>(pb, w, x0, x1, l, &its, B, s);
         if (Uk && l < N) Uk[(s * k_sim + kk) * N + l] = w.U()[l];

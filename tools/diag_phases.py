@@ -14,8 +14,10 @@ buf = (C.c_ulonglong * 48)()
 x = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(0, B))
 rho, uo = ctl.initial_state(x, cfg)
 ws = ctl.new_active_ws(B, cfg)
-out = ctl.step(x, rho, uo, cfg, active_ws=ws); torch.cuda.synchronize()
-x = out["x_next"].clone()
+WARM = int(sys.argv[4]) if len(sys.argv) > 4 else 6   # steps before the measured one (bench: 5 warmup)
+for _ in range(WARM):
+    out = ctl.step(x, rho, uo, cfg, active_ws=ws); torch.cuda.synchronize()
+    x = out["x_next"].clone()
 lib.ntm_debug_stamps(buf, 1)
 t = time.time()
 out = ctl.step(x, rho, uo, cfg, active_ws=ws); torch.cuda.synchronize()
@@ -23,7 +25,7 @@ dt = time.time() - t
 assert lib.ntm_debug_stamps(buf, 1) == 0
 names = "lift cost scale cand regram gi polish roll gi_fact gi_check gi_dir gi_add gi_drop".split()
 tot = sum(buf[i] for i in range(8))
-print(f"B={B} step {dt*1e3:.1f} ms; cycles per wave-step by phase (s_memtime):")
+print(f"B={B} N={N} step {WARM + 1} {dt*1e3:.1f} ms; cycles per wave-step by phase (s_memtime):")
 for i, n in enumerate(names):
     print(f"  {n:9s} {buf[i]/B:12.0f}  {100*buf[i]/tot:5.1f}%")
 print(f"per wave-step: check calls {buf[13]/B:.1f}, candidate sets {buf[14]/B:.2f}, hits {buf[15]/B:.2f} (after repair {buf[22]/B:.2f}), GI solves {buf[23]/B:.2f}")
@@ -40,3 +42,4 @@ print(f"per wave-step: tries it=1 {buf[37]/B:.2f} failed {buf[32]/B:.2f}; tries 
       f"GI solves at it=1 {buf[34]/B:.2f}, it=2 {buf[35]/B:.2f}, later {buf[36]/B:.2f}")
 print(f"per wave-step: GI warm starts tried {buf[39]/B:.2f}, accepted {buf[40]/B:.2f}")
 print(f"  dependent rows skipped {buf[41]/B:.3f}; rejected: negative multiplier {buf[42]/B:.3f}; stopped at N rows {buf[43]/B:.3f}")
+print(f"per wave-step: shifted second candidate at it=2 tried {buf[44]/B:.2f}, hits {buf[45]/B:.2f}")
