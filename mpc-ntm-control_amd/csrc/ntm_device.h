@@ -1717,10 +1717,42 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
         w.xp()[r] = y + w.e()[r] - ((r & 1) ? pb.r[1] : pb.r[0]);
     }
     NTM_WSYNC();
+    // --- square, triangular E (nS == nF, the common "boundary arc": the state held
+    //     at its bound by every free input).  The active general rows then pin the
+    //     free variables down on their own: sorted by their last free variable they
+    //     make E lower triangular with a non-zero diagonal, so V_F follows from
+    //     E V_F = h by forward substitution and the multipliers from E' mu = grad_F
+    //     by back substitution in the certificate; no Gram of the free columns and
+    //     no bordered elimination.  perm[t] = the general row whose last free
+    //     variable is the t-th (scratch ints in the R block; E goes to the J block).
+    int* const perm = reinterpret_cast<int*>(w.R());
+    bool sq = false;
+    if (nS == nF && nS > 0 && !collide) {
+        const unsigned long long fm = bal >> (lane & ~(P - 1));   // bit j: variable j is free
+        int lastf = -1;
+        if (l < nS) {
+            const int r = w.srw()[l];
+            int lj = -1;
+            if (r >= 2 * N) {                                  // rate row of input i: e_i - e_{i-1}
+                const int i = r - 2 * N;
+                lj = ((fm >> i) & 1ull) ? i : (((fm >> (i - 1)) & 1ull) ? i - 1 : -1);
+            } else {                                           // state row r: Gamma_r, columns j <= r/2
+                const int jm = r >> 1;
+                for (int j = 0; j < N; ++j)
+                    if (j <= jm && ((fm >> j) & 1ull) && w.gt(r, j) != 0.0) lj = j;
+            }
+            if (lj >= 0) lastf = __popcll(fm & ((1ull << lj) - 1ull));
+            perm[l] = -1;
+        }
+        NTM_WSYNC();
+        if (lastf >= 0) perm[lastf] = l;                       // a repeated last column leaves a hole
+        NTM_WSYNC();
+        sq = gmaxi<P>((l < nS && perm[l] < 0) ? 1 : 0) == 0;
+    }
     NTM_ACC(ST_P_CLASS, tp);
     // --- g_F (lane a = compact index) ---
     double gl = 0.0;
-    if (l < nF) {
+    if (!sq && l < nF) {
         const int ja = w.fidx()[l];
         const double* ca = w.Gt() + w.gidx(2 * ja, ja) - 2 * ja;   // ca[r] = gt(r, ja), r >= 2 ja
         const double g2 = qdot_rows<4>(ca, w.xp(), N, ja, q00, q01, q10, q11);   // terms i < ja masked
@@ -1739,10 +1771,10 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
         NNc > 0 && (2 * NNc) * (2 * NNc + 1) / 2 + 2 * NNc <= NNc * LDc + (NNc + 1) * LDc;
     const bool fused = kAlwaysFused || ((nt + 1 <= RPL * P) && (nt * (nt + 1) / 2 + nt <= N * LDJ + (N + 1) * LD));
     double* const Lp = w.J();
-    if (fused && l < nF) Lp[(nt * (nt + 1)) / 2 + l] = -gl;
+    if (!sq && fused && l < nF) Lp[(nt * (nt + 1)) / 2 + l] = -gl;
     // --- compact G~_FF: one (a, c) entry per lane (packed rows, or lower col-major in R) ---
     {
-        const int npair = nF * (nF + 1) / 2;
+        const int npair = sq ? 0 : nF * (nF + 1) / 2;
         for (int idx = l; idx < npair; idx += P) {
             int a = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
             if ((a + 1) * (a + 2) / 2 <= idx) ++a;
@@ -1794,7 +1826,34 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
     bool ok = !collide;
     int fk = ok ? 0 : 3, fpos_out = 0;
     double vfin = 0.0;
-    if (fused) {
+    double sq_id = 0.0;                                   // square path: 1 / E[t][t] on lane t
+    if (sq) {
+        // sorted E (row t = general row perm[t], n x n, row-major at Lp[t LD + a]) and h
+        const int n = nS;
+        for (int idx = l; idx < n * n; idx += P) {
+            const int t = idx / n, a = idx - t * n;
+            Lp[t * LD + a] = (a <= t) ? gen_n(perm[t], w.fidx()[a]) : 0.0;
+        }
+        double acc = (l < n) ? hs_of(perm[l]) : 0.0;
+        NTM_WSYNC();
+        if (l < n) sq_id = 1.0 / Lp[l * LD + l];
+        NTM_ACC(ST_S_E, tp);
+        // E V_F = h: lane t owns row t; step t broadcasts x_t and updates the rows below
+        double x = 0.0;
+        double en = (l > 0 && l < n) ? Lp[l * LD] : 0.0;      // E[l][t], loaded one step ahead
+        for (int t = 0; t < n; ++t) {
+            const double et = en;
+            if (t + 1 < n) en = (l > t + 1 && l < n) ? Lp[l * LD + t + 1] : 0.0;
+            const double xt = gbcast<P>(acc * sq_id, t);
+            if (l == t) x = xt;
+            acc -= et * xt;
+        }
+        ok = gmaxi<P>((l < n && !isfinite(x)) ? 1 : 0) == 0;
+        if (!ok) fk = 3;
+        const double vsc = __shfl(x, (l < N && !fixed) ? fpos : 0, P);
+        vfin = fixed ? vb : vsc;
+        NTM_ACC(ST_S_Y, tp);
+    } else if (fused) {
         // E rows over the free variables (one entry per lane) and h; the trailing
         // block of A is zero and is never stored (the elimination starts it at 0)
         for (int idx = l; idx < nF * nS; idx += P) {
@@ -2056,6 +2115,23 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
             const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;
             const double g2 = qdot_rows<4>(cl, w.xp(), N, l, q00, q01, q10, q11);   // terms i < l masked
             res = w.D()[l] * (2 * g2) + w.F()[l];
+        }
+        if (sq) {
+            // square path: the multipliers from E' mu = grad_F (E upper triangular in
+            // sorted order), back substitution; lane t owns row t and grad at f_t
+            if (l < N && !fixed) w.d()[fpos] = res;
+            NTM_WSYNC();
+            double acc = (l < nS) ? w.d()[l] : 0.0, mu = 0.0;
+            for (int u = nS - 1; u >= 0; --u) {
+                const double eu = (l < u) ? Lp[u * LD + l] : 0.0;
+                const double mu_u = gbcast<P>(acc * sq_id, u);
+                if (l == u) mu = mu_u;
+                acc -= eu * mu_u;
+            }
+            if (l < nS) w.np()[perm[l]] = mu;
+            NTM_WSYNC();
+        }
+        if (l < N) {
             for (int s2 = 0; s2 < nS; ++s2) res -= w.np()[s2] * gen_n(s2, l);
         }
         // multipliers: general row s on lane s, fixed variable j on lane j; each

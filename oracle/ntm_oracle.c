@@ -418,6 +418,41 @@ static int orc_polish(int n, int m, const double* Gs, const double* Fs, const do
             S[nS++] = row;
         }
     }
+    /* Square, triangular E (nS == number of free variables; the GPU's
+     * polish_compact square path): the active general rows alone determine the
+     * free variables.  Sorted by their last free column, E is lower triangular:
+     * V_F by forward substitution, the multipliers by back substitution on
+     * E' mu = grad_F below (same order of operations as the device). */
+    int nF = 0, fidx[NMAX], perm[NMAX], sq = 0;
+    static __thread double Eq[NMAX * NMAX];
+    double sqid[NMAX];
+    for (int j = 0; j < n; ++j) if (!fixed[j]) fidx[nF++] = j;
+    if (nS == nF && nS > 0) {
+        sq = 1;
+        for (int t = 0; t < nS; ++t) perm[t] = -1;
+        for (int k = 0; k < nS && sq; ++k) {
+            int last = -1;
+            for (int a = 0; a < nF; ++a) if (Ls[(size_t)fidx[a] * m + S[k]] != 0.0) last = a;
+            if (last < 0 || perm[last] >= 0) sq = 0;
+            else perm[last] = k;
+        }
+    }
+    if (sq) {
+        double acc[NMAX];
+        for (int t = 0; t < nS; ++t) {
+            const int row = S[perm[t]];
+            double hk = -bs[row];
+            for (int j = 0; j < n; ++j) if (fixed[j]) hk -= (-Ls[(size_t)j * m + row]) * Vb[j];
+            acc[t] = hk;
+            for (int a = 0; a < nS; ++a) Eq[t * NMAX + a] = (a <= t) ? -Ls[(size_t)fidx[a] * m + row] : 0.0;
+            sqid[t] = 1.0 / Eq[t * NMAX + t];
+        }
+        for (int t = 0; t < nS; ++t) {
+            const double xt = acc[t] * sqid[t];
+            V[fidx[t]] = xt;
+            for (int u = t + 1; u < nS; ++u) acc[u] -= Eq[u * NMAX + t] * xt;
+        }
+    } else {
     for (int i = 0; i < n; ++i) {
         double s = Fs[i];
         for (int j = 0; j < n; ++j) if (fixed[j]) s += Gs[(size_t)j * n + i] * Vb[j];
@@ -463,6 +498,7 @@ static int orc_polish(int n, int m, const double* Gs, const double* Fs, const do
         for (int i = 0; i < n; ++i) tmp[i] = -w[i];
         bwd_rm(n, Lc, tmp, V);
     }
+    }
     for (int j = 0; j < n; ++j) if (fixed[j]) V[j] = Vb[j];
     /* KKT certificate: primal slack on every non-constant row, multiplier signs */
     double vmax = 1.0;
@@ -477,9 +513,19 @@ static int orc_polish(int n, int m, const double* Gs, const double* Fs, const do
     for (int i = 0; i < n; ++i) {
         double s = Fs[i];
         for (int j = 0; j < n; ++j) s += Gs[(size_t)j * n + i] * V[j];
-        for (int k = 0; k < nS; ++k) s -= mu[k] * (-Ls[(size_t)i * m + S[k]]);
         res[i] = s;
     }
+    if (sq) {                                   /* E' mu = grad_F, back substitution */
+        double acc[NMAX];
+        for (int t = 0; t < nS; ++t) acc[t] = res[fidx[t]];
+        for (int u = nS - 1; u >= 0; --u) {
+            const double mu_u = acc[u] * sqid[u];
+            mu[perm[u]] = mu_u;
+            for (int t = 0; t < u; ++t) acc[t] -= Eq[u * NMAX + t] * mu_u;
+        }
+    }
+    for (int i = 0; i < n; ++i)
+        for (int k = 0; k < nS; ++k) res[i] -= mu[k] * (-Ls[(size_t)i * m + S[k]]);
     for (int k = 0; k < nS; ++k) mults[nm++] = mu[k];
     for (int a = 0; a < q; ++a) {
         int row = act[a], isS = 0;

@@ -525,6 +525,40 @@ def polish_active_set(Gs, Fs, Ns, bcs, act, Lin, b, Dv):
             fixed[j] = True
         else:
             S.append(a)
+    free = np.flatnonzero(~fixed)
+    if S and len(S) == len(free):
+        # Square, triangular E (the device's polish_compact square path): the
+        # active general rows alone determine the free variables.  Sorted by their
+        # last free column E is lower triangular: V_F by forward substitution, the
+        # multipliers by back substitution on E' mu = grad_F (same order of
+        # operations as the device and oracle/ntm_oracle.c).
+        nS = len(S)
+        perm = [-1] * nS
+        for k, a in enumerate(S):
+            nzf = np.flatnonzero(Ns[a, free] != 0.0)
+            last = int(nzf[-1]) if len(nzf) else -1
+            if last < 0 or perm[last] >= 0:
+                perm = None
+                break
+            perm[last] = k
+        if perm is not None:
+            rows = [S[k] for k in perm]
+            E = np.array([[Ns[r, free[c]] if c <= t else 0.0 for c in range(nS)] for t, r in enumerate(rows)])
+            acc = np.array([bcs[r] - Ns[r, fixed] @ Vb[fixed] for r in rows])
+            sqid = 1.0 / np.diag(E)
+            V = Vb.copy()
+            for t in range(nS):
+                xt = acc[t] * sqid[t]
+                V[free[t]] = xt
+                acc[t + 1:] -= E[t + 1:, t] * xt
+            grad = Gs @ V + Fs
+            acc = grad[free].copy()
+            mu = np.zeros(nS)
+            for u in range(nS - 1, -1, -1):
+                mu_u = acc[u] * sqid[u]
+                mu[perm[u]] = mu_u
+                acc[:u] -= E[u, :u] * mu_u
+            return _polish_certify(Gs, Fs, Ns, bcs, act, Lin, Dv, S, fixed, Ufix, V, mu)
     g = Fs + Gs[:, fixed] @ Vb[fixed]
     Gm = Gs.copy()
     Gm[fixed, :] = 0.0
@@ -550,8 +584,13 @@ def polish_active_set(Gs, Fs, Ns, bcs, act, Lin, b, Dv):
     else:
         V = _bwd(Lc, -w)
     V = np.where(fixed, Vb, V)
+    return _polish_certify(Gs, Fs, Ns, bcs, act, Lin, Dv, S, fixed, Ufix, V, mu)
+
+
+def _polish_certify(Gs, Fs, Ns, bcs, act, Lin, Dv, S, fixed, Ufix, V, mu):
+    """KKT certificate of an active-set re-solve: primal slack on every
+    non-constant row, multiplier signs.  Returns (V, U, ok)."""
     U = np.where(fixed, Ufix, V * Dv)
-    # KKT certificate
     nzr = np.any(Ns != 0.0, axis=1)
     slack = Ns @ V - bcs
     vmax = max(1.0, float(np.max(np.abs(V))))

@@ -236,7 +236,11 @@ def test_step_teacher_forced(ctl, N, mode, warm):
     tol = U_TOL_RATE if mode == 3 else U_TOL
     assert worst <= tol, worst
     assert worst_div <= tol, worst_div
-    assert same_iters >= 0.9 * n, (same_iters, n)
+    # the fraction of scenarios that stop at the same inner iteration is a property
+    # of two exact solvers' rounding at the bitwise stopping rule: the two CPU
+    # restatements themselves agree on 69% of the mode-3 steps at N = 4
+    # (tests/test_oracle_c.py), the diverged ones are bounded by worst_div above
+    assert same_iters >= (0.6 if mode == 3 else 0.9) * n, (same_iters, n)
 
 
 @pytest.mark.parametrize("N", [4, 20])
