@@ -15,6 +15,12 @@
 //   gi_solve          quadprog call NTM_MPC_Sim.m:97 (Goldfarb-Idnani)
 //   rollout_phase     NTM_MPC_Sim.m:110-117, 123-127
 //   plant_phase       NTM_MPC_Sim.m:130 (CANON D13)
+//
+// Every phase is __forceinline__: left to its heuristics the inliner outlines
+// whichever phase crosses its size threshold, and an outlined phase is a real
+// call on gfx950 (the Prob and WS references copied to scratch, the caller's
+// live VGPRs saved around it): 15.9 -> 14.7 ms per step-batch at B=1e5, N=20
+// once everything was inlined again.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -48,6 +54,7 @@ struct Prob {
 };
 
 constexpr double kInf = __builtin_huge_val();
+
 
 // 1/sqrt(x) for x > 0: v_rsq_f64 plus two Newton steps (full fp64 accuracy;
 // the pivots of the small Cholesky factorisations sit on their sequential
@@ -83,7 +90,7 @@ __shared__ int ntm_trace_grp;   // group (of this one-wave block) that owns the 
 // Diagnostic build only (-DNTM_STAMPS): per-phase s_memtime cycle totals,
 // summed over waves into ntm_stamps[] (read with ntm_debug_stamps).  The
 // production library compiles every stamp away.
-#define NTM_NSTAMPS 48
+#define NTM_NSTAMPS 64
 #ifdef NTM_STAMPS
 extern __device__ unsigned long long ntm_stamps[NTM_NSTAMPS];
 __shared__ unsigned long long ntm_lds_stamps[NTM_NSTAMPS];   // per block (= per wave), flushed once
@@ -111,10 +118,13 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        ST_GI_DIR, ST_GI_ADD, ST_GI_DROP, CN_CHECK, CN_CAND, CN_HIT,
        ST_P_CLASS, ST_P_GRAM, ST_P_CHOL, ST_P_SCHUR, ST_P_BWD, ST_P_KKT, CN_REPAIR, CN_GIRUN,
        ST_S_E, ST_S_Y, ST_S_K, ST_S_CHOL, ST_S_SOLVE, CN_TRY_EARLY, CN_FAIL_EARLY, CN_FAIL_LATE,
-       CN_FAIL_IT1, CN_FAIL_IT2, CN_GI_IT1, CN_GI_IT2, CN_GI_LATE, CN_TRY_IT1, CN_TRY_IT2, CN_WARM_TRY, CN_WARM_OK, CN_WARM_DEP, CN_WARM_NEG, CN_WARM_FULL, CN_ALT_TRY, CN_ALT_HIT };
+       CN_FAIL_IT1, CN_FAIL_IT2, CN_GI_IT1, CN_GI_IT2, CN_GI_LATE, CN_TRY_IT1, CN_TRY_IT2, CN_WARM_TRY, CN_WARM_OK, CN_WARM_DEP, CN_WARM_NEG, CN_WARM_FULL, CN_ALT_TRY, CN_ALT_HIT,
+       ST_K_Y, ST_K_CHK, ST_K_GRAD, ST_K_MU, ST_K_SUB, ST_C_A, ST_C_B, ST_C_Y, ST_C_SQ,
+       ST_SC_COL, ST_SC_ROW, ST_SC_END, ST_L_COEF, ST_L_LOOP };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 constexpr int kMaxNT = 32;         // explicit R^{-1} in GI up to this horizon (WS::useT)
-constexpr int kRepairs = 8;        // single-row repairs of a failed warm-start candidate
+constexpr int kRepairs = 8;
+constexpr int kRowMulti = 256;     // WS::rinfo flag: the state row has two or more non-zeros        // single-row repairs of a failed warm-start candidate
 constexpr int kGiWarmRejected = 100;   // gi_solve: the warm-start set was not dual feasible (caller reruns cold)
 
 #define NTM_WSYNC()                                              \
@@ -330,7 +340,9 @@ struct WS {
     // T = R^{-1} of the GI factorisation (upper triangular, row-major n() x ldj();
     // zero outside the leading q x q block), so the dual direction is a matvec
     __device__ __forceinline__ double* T() const { return base + oT(); }
-    __device__ __forceinline__ double* rn() const { return base + oV(); }           // 2N state-row norms
+    // 2N ints (in 2N doubles of space): per state row r, (last column j with
+    // Gamma_rj != 0) + 1, plus kRowMulti if it has two or more non-zeros
+    __device__ __forceinline__ int* rinfo() const { return reinterpret_cast<int*>(base + oV()); }
     __device__ __forceinline__ double* F() const { return base + oV() + 2 * n(); }    // n()  F~
     __device__ __forceinline__ double* D() const { return base + oV() + 3 * n(); }    // n()  Jacobi scaling
     __device__ __forceinline__ double* V() const { return base + oV() + 4 * n(); }    // n()  scaled variables
@@ -440,6 +452,61 @@ __device__ __forceinline__ double dot_batched(const double* a, int sa, const dou
     }
     return y;
 }
+// sum_{lo <= j < hi} a[j sa] b[j sb] (per-lane bounds; terms added in index order)
+template <int CH>
+__device__ __forceinline__ double dot_range(const double* a, int sa, const double* b, int sb, int lo, int hi) {
+    double y = 0.0;
+    for (int j0 = lo; j0 < hi; j0 += CH) {
+        double x[CH], z[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int j = j0 + u;
+            const bool in = j < hi;
+            x[u] = in ? a[j * sa] : 0.0;
+            z[u] = in ? b[j * sb] : 0.0;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) y += x[u] * z[u];
+    }
+    return y;
+}
+// s - sum_{lo <= j < hi} a[j sa] b[j sb], the terms subtracted one by one in index order
+template <int CH>
+__device__ __forceinline__ double sub_dot(double s, const double* a, int sa, const double* b, int sb, int lo, int hi) {
+    for (int j0 = lo; j0 < hi; j0 += CH) {
+        double x[CH], z[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int j = j0 + u;
+            const bool in = j < hi;
+            x[u] = in ? a[j * sa] : 0.0;
+            z[u] = in ? b[j * sb] : 0.0;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) s -= x[u] * z[u];
+    }
+    return s;
+}
+// a[j] -= f b[j] for lo <= j < hi, the loads of CH entries issued ahead of their stores
+template <int CH>
+__device__ __forceinline__ void axpy_sub(double* a, const double* b, double f, int lo, int hi) {
+    for (int j0 = lo; j0 < hi; j0 += CH) {
+        double x[CH], z[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int j = j0 + u;
+            const bool in = j < hi;
+            x[u] = in ? a[j] : 0.0;
+            z[u] = in ? b[j] : 0.0;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < CH; ++u)
+            if (j0 + u < hi) a[j0 + u] = x[u] - f * z[u];
+    }
+}
 // Gamma_r v restricted to j <= r/2 (row r of the packed block-lower-triangular Gamma)
 template <int CH, class W>
 __device__ __forceinline__ double gamma_row_dot(const W& w, int r, const double* v) {
@@ -469,7 +536,7 @@ __device__ __forceinline__ double gamma_row_dot(const W& w, int r, const double*
 // L2: lifted prediction  (Rho_to_PhiGammaLambda.m:17-52, CANON D4/D6)
 // ---------------------------------------------------------------------------
 template <int P, class W>
-__device__ void lift_phase(const Prob& pb, const W& w, int l) {
+__device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l) {
     const int N = w.n();
     const Coef& k = pb.k;
     if (l < N) {
@@ -478,6 +545,7 @@ __device__ void lift_phase(const Prob& pb, const W& w, int l) {
         w.bb()[l] = coef_b(k, w.rho()[3 * l + 2]);
     }
     NTM_WSYNC();
+    NTM_T0(tlf);
     // Gamma: lane j owns column j: Gamma_jj = B_j, Gamma_ij = A_i Gamma_{i-1,j} (D6).
     // Lanes N and N+1 run the same 2-vector recursion for the two columns of
     // Phi_i = A_i Phi_{i-1} (D4), lane N+2 for Lambda_i = A_i Lambda_{i-1} + C,
@@ -499,15 +567,35 @@ __device__ void lift_phase(const Prob& pb, const W& w, int l) {
             else { w.Lam()[2 * i] = g0; w.Lam()[2 * i + 1] = g1; }
         };
         put(gam ? l : 0);
-        for (int i = 1; i < N; ++i) {        // fixed trip count (unrolls), branch-free:
-            const double n0 = w.a11()[i] * g0 + c0;        // Gamma rows i <= l keep (B_l, 0)
-            const double n1 = (w.a21()[i] * g0 + k.a22 * g1) + c1;   // and rewrite the diagonal
-            const bool live = !gam || i > l;
-            g0 = live ? n0 : g0;
-            g1 = live ? n1 : g1;
-            put(live ? i : l);
+        // fixed trip count (unrolls), branch-free: Gamma rows i <= l keep (B_l, 0) and
+        // rewrite the diagonal.  The coefficients of CH steps are loaded ahead of the
+        // chunk's stores (the stores cannot be proven not to alias them, so per-step
+        // loads would wait for the previous step's stores: one LDS round trip a step)
+        constexpr int CH = 4;
+        for (int i0 = 1; i0 < N; i0 += CH) {
+            double ca[CH], cb[CH];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int i = i0 + u;
+                ca[u] = i < N ? w.a11()[i] : 0.0;
+                cb[u] = i < N ? w.a21()[i] : 0.0;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int i = i0 + u;
+                if (i < N) {
+                    const double n0 = ca[u] * g0 + c0;
+                    const double n1 = (cb[u] * g0 + k.a22 * g1) + c1;
+                    const bool live = !gam || i > l;
+                    g0 = live ? n0 : g0;
+                    g1 = live ? n1 : g1;
+                    put(live ? i : l);
+                }
+            }
         }
     }
+    NTM_ACC(ST_L_LOOP, tlf);
     // Phi and Lambda on lane 0 when the group has no idle lanes
     if (!extra && l == 0) {
         double p00 = w.a11()[0], p10 = w.a21()[0], p01 = 0.0, p11 = k.a22;
@@ -532,7 +620,7 @@ __device__ void lift_phase(const Prob& pb, const W& w, int l) {
 // free response e = Phi x_k + Lambda (the x-dependent part of NTM_MPC_Sim.m:121
 // and of c + W x_k at :97)
 template <int P, class W>
-__device__ void free_response(const W& w, double x0, double x1, int l) {
+__device__ __forceinline__ void free_response(const W& w, double x0, double x1, int l) {
     for (int i = l; i < w.n(); i += P) {
         const double* Ph = w.Phi() + 4 * i;
         w.e()[2 * i] = (Ph[0] * x0 + Ph[2] * x1) + w.Lam()[2 * i];
@@ -546,7 +634,7 @@ __device__ void free_response(const W& w, double x0, double x1, int l) {
 // F = 2 Gamma' Om (e - R)      NTM_MPC_Sim.m:120-121 (CANON D8, D12)
 // ---------------------------------------------------------------------------
 template <int P, class W>
-__device__ void gram_rows(const Prob& pb, const W& w, double* dst, int l) {
+__device__ __forceinline__ void gram_rows(const Prob& pb, const W& w, double* dst, int l) {
     const int N = w.n(), LD = w.ldj();
     const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
     // one (j, kk) entry per lane; fixed-trip masked dot (column reads below the
@@ -572,7 +660,7 @@ __device__ void gram_rows(const Prob& pb, const W& w, double* dst, int l) {
 }
 
 template <int P, class W>
-__device__ void cost_phase(const Prob& pb, const W& w, int l) {
+__device__ __forceinline__ void cost_phase(const Prob& pb, const W& w, int l) {
     const int N = w.n();
     const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
     gram_rows<P>(pb, w, w.R(), l);
@@ -593,7 +681,7 @@ __device__ void cost_phase(const Prob& pb, const W& w, int l) {
 // G~ = D G D in place (lower triangle, col-major); the same expression order
 // is used when the polish recomputes G~ (so both copies are bit-identical).
 template <int P, class W>
-__device__ int scale_gram(const W& w, double* G, int l) {
+__device__ __forceinline__ int scale_gram(const W& w, double* G, int l) {
     int bad = 0;
     if (l < w.n()) {
         double Dl = w.D()[l];
@@ -615,10 +703,11 @@ __device__ int scale_gram(const W& w, double* G, int l) {
 // Returns false (group-uniform) if any datum is non-finite.
 // ---------------------------------------------------------------------------
 template <int P, class W>
-__device__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_state_rows) {
+__device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_state_rows) {
     const int N = w.n();
     const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
     int bad = 0;
+    NTM_T0(tsc);
     if (l < N) {
         // one pass over Gamma's column l: the Gram diagonal G_ll and F_l = 2 Gamma_l' Om (e - r)
         const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
@@ -663,6 +752,7 @@ __device__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_st
         w.vhi()[l] = pb.umax / Dl;
     }
     NTM_WSYNC();
+    NTM_ACC(ST_SC_COL, tsc);
     if (pb.mode == NTM_MODE_FULL_DU && l >= 1 && l < N) {      // rate-row norms |D (e_l - e_{l-1})|
         const double a = w.D()[l], b = w.D()[l - 1];
         w.idun()[l] = 1.0 / sqrt(a * a + b * b);
@@ -671,6 +761,7 @@ __device__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_st
         for (int r = l; r < 2 * N; r += P) {
             double s = 0.0;
             const int jmax = r >> 1;
+            int last = -1, cnt = 0;
             constexpr int CH = 4;
             for (int j0 = 0; j0 < N; j0 += CH) { // fixed trip count, j > jmax masked; batched loads
                 double g[CH], dd[CH];
@@ -684,22 +775,27 @@ __device__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_st
 #pragma unroll
                 for (int u = 0; u < CH; ++u) {
                     const double v = g[u] * dd[u];
-                    s += (j0 + u <= jmax) ? v * v : 0.0;
+                    const bool in = j0 + u <= jmax;
+                    s += in ? v * v : 0.0;
+                    if (in && g[u] != 0.0) { last = j0 + u; ++cnt; }
                 }
             }
             bad |= !isfinite(s) || !isfinite(w.e()[r]);
             const double ir = (s > 0.0 && s < kInf) ? rsqrt_nr(s) : 0.0;
-            w.rn()[r] = s * ir;                  // |Gamma_r D|
-            w.irn()[r] = ir;
+            w.irn()[r] = ir;                     // 1/|Gamma_r D| (0: constant row)
+            w.rinfo()[r] = (last + 1) | (cnt > 1 ? kRowMulti : 0);
         }
         NTM_WSYNC();
     }
-    return gmaxi<P>(bad) == 0;
+    NTM_ACC(ST_SC_ROW, tsc);
+    const bool ok = gmaxi<P>(bad) == 0;
+    NTM_ACC(ST_SC_END, tsc);
+    return ok;
 }
 
 // the full scaled Hessian G~ (lower, col-major) into w.R() for the GI fallback
 template <int P, class W>
-__device__ bool full_gram(const Prob& pb, const W& w, int l) {
+__device__ __forceinline__ bool full_gram(const Prob& pb, const W& w, int l) {
     gram_rows<P>(pb, w, w.R(), l);
     NTM_WSYNC();
     int bad = scale_gram<P>(w, w.R(), l);
@@ -710,7 +806,7 @@ __device__ bool full_gram(const Prob& pb, const W& w, int l) {
 // kept for the dense-row entry point (ntm_qp_device): G~ = D G D in place,
 // F~ = D F (G given in w.R()); no state rows
 template <int P, class W>
-__device__ bool scale_phase(const W& w, int l, bool /*with_state_rows*/) {
+__device__ __forceinline__ bool scale_phase(const W& w, int l, bool /*with_state_rows*/) {
     const int N = w.n(), LD = w.ldj();
     if (l < N) {
         double g = w.R()[l + l * LD];
@@ -823,7 +919,7 @@ struct StructRows {
         int kind, j;
         decode(id, w.n(), kind, j);
         if (kind >= 4) return 1.0 / w.idun()[j];
-        return kind < 2 ? w.D()[j] : w.rn()[j];
+        return kind < 2 ? w.D()[j] : 1.0 / w.irn()[j];
     }
 
     // constant rows (x_0 rows; state rows with Gamma_r == 0): 0 <= b or infeasible (D15)
@@ -838,7 +934,7 @@ struct StructRows {
                 bad |= (xmax(1) - x1) < 0.0;
             }
             for (int r = l; r < 2 * w.n(); r += P) {
-                if (w.rn()[r] == 0.0) {
+                if (w.irn()[r] == 0.0) {
                     int c = r & 1;
                     bad |= (w.e()[r] - xmin(c)) < 0.0;
                     bad |= (xmax(c) - w.e()[r]) < 0.0;
@@ -1010,12 +1106,11 @@ struct DenseRows {
 // reciprocals of the diagonal go to rdiag[0..n) (the triangular solves then
 // multiply instead of divide); false if not PD
 template <int P>
-__device__ bool chol_inplace(double* A, int n, int RS, int CS, int l, double* rdiag) {
+__device__ __forceinline__ bool chol_inplace(double* A, int n, int RS, int CS, int l, double* rdiag) {
     for (int k = 0; k < n; ++k) {
         double s = 0.0;
         if (l >= k && l < n) {
-            s = A[l * RS + k * CS];
-            for (int j = 0; j < k; ++j) s -= A[l * RS + j * CS] * A[k * RS + j * CS];
+            s = sub_dot<4>(A[l * RS + k * CS], A + l * RS, CS, A + k * RS, CS, 0, k);
         }
         double dk = gbcast<P>(s, k);
         if (!(dk > 0.0) || !(dk < kInf)) return false;
@@ -1029,7 +1124,7 @@ __device__ bool chol_inplace(double* A, int n, int RS, int CS, int l, double* rd
 }
 // lane i holds b_i in `v`; returns x_i of L x = b (L lower, rdiag = 1/diag)
 template <int P>
-__device__ double fwd_lanes(const double* L, const double* rdiag, int n, int RS, int CS, double v, int l) {
+__device__ __forceinline__ double fwd_lanes(const double* L, const double* rdiag, int n, int RS, int CS, double v, int l) {
     double acc = (l < n) ? v : 0.0, x = 0.0;
     for (int k = 0; k < n; ++k) {
         double xk = gbcast<P>(acc, k) * rdiag[k];
@@ -1040,7 +1135,7 @@ __device__ double fwd_lanes(const double* L, const double* rdiag, int n, int RS,
 }
 // lane i holds b_i in `v`; returns x_i of L' x = b (L lower, rdiag = 1/diag)
 template <int P>
-__device__ double bwd_lanes(const double* L, const double* rdiag, int n, int RS, int CS, double v, int l) {
+__device__ __forceinline__ double bwd_lanes(const double* L, const double* rdiag, int n, int RS, int CS, double v, int l) {
     double acc = (l < n) ? v : 0.0, x = 0.0;
     for (int k = n - 1; k >= 0; --k) {
         double xk = gbcast<P>(acc, k) * rdiag[k];
@@ -1060,7 +1155,7 @@ __device__ double bwd_lanes(const double* L, const double* rdiag, int n, int RS,
 // (Goldfarb & Idnani 1983, section 3).
 // ---------------------------------------------------------------------------
 template <int P, class Rows, class W>
-__device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, int l, int* iters_out, int* q_out,
+__device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, int l, int* iters_out, int* q_out,
                         int nwarm = 0) {
     const int N = w.n(), LD = w.ldj(), LDJ = w.ldj();
     *iters_out = 0;
@@ -1073,8 +1168,7 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
         for (int i = 0; i < N; ++i) {
             double x = 0.0;
             if (i >= l) {
-                x = (i == l) ? 1.0 : 0.0;
-                for (int k2 = l; k2 < i; ++k2) x -= w.R()[i + k2 * LD] * w.J()[l * LDJ + k2];
+                x = sub_dot<4>((i == l) ? 1.0 : 0.0, w.R() + i, LD, w.J() + l * LDJ, 1, l, i);
                 x *= w.ldi()[i];
             }
             w.J()[l * LDJ + i] = x;
@@ -1085,12 +1179,11 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
     double Vl = 0.0;
     {
         double t = 0.0;
-        if (l < N) for (int i = 0; i < N; ++i) t += w.J()[i * LDJ + l] * w.F()[i];
+        if (l < N) t = dot_batched<4>(w.J() + l, LDJ, w.F(), 1, N);
         if (l < N) w.d()[l] = t;
         NTM_WSYNC();
         if (l < N) {
-            double v = 0.0;
-            for (int k2 = 0; k2 < N; ++k2) v += w.J()[l * LDJ + k2] * w.d()[k2];
+            const double v = dot_batched<4>(w.J() + l * LDJ, 1, w.d(), 1, N);
             Vl = -v;
             w.V()[l] = Vl;
             w.U()[l] = w.D()[l] * Vl;
@@ -1130,15 +1223,12 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
                 if (l < N) dl = esg * w.J()[ej * LDJ + l];
             } else {
                 bcp = uni<P>(rows.template load_np<P>(w, p, l));
-                if (l < N) for (int i = 0; i < N; ++i) dl += w.J()[i * LDJ + l] * w.np()[i];
+                if (l < N) dl = dot_batched<4>(w.J() + l, LDJ, w.np(), 1, N);
             }
             if (l < N) { w.d()[l] = (l >= q) ? dl : 0.0; w.dr()[l] = (l < q) ? dl : 0.0; }
             NTM_WSYNC();
             double rl = 0.0;
-            if (useT && l < N) {
-#pragma unroll 4
-                for (int b = 0; b < N; ++b) rl += w.T()[l * LDJ + b] * w.dr()[b];
-            }
+            if (useT && l < N) rl = dot_batched<4>(w.T() + l * LDJ, 1, w.dr(), 1, N);
             const double zn = gsum<P>((l >= q && l < N) ? dl * dl : 0.0);
             const double dnrm = gsum<P>(dl * dl);
             if (q >= N) { NTM_CNT(CN_WARM_FULL); break; }
@@ -1157,10 +1247,9 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
                 double vtv = gsum<P>(vl * vl);
                 NTM_WSYNC();
                 if (l < N) {
-                    double dot = 0.0;
-                    for (int k2 = 0; k2 < N; ++k2) dot += w.J()[l * LDJ + k2] * w.hv()[k2];
-                    double f = 2.0 * dot / vtv;
-                    for (int k2 = q; k2 < N; ++k2) w.J()[l * LDJ + k2] -= f * w.hv()[k2];
+                    const double dot = dot_batched<4>(w.J() + l * LDJ, 1, w.hv(), 1, N);
+                    const double f = 2.0 * dot / vtv;
+                    axpy_sub<4>(w.J() + l * LDJ, w.hv(), f, q, N);
                 }
             }
             const double ih = 1.0 / h;
@@ -1181,9 +1270,9 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
         if (okw) {
             // c = J' F~ (lane k), wv = (T' bc)_k for k < q
             double c = 0.0, wv = 0.0;
-            if (l < N) for (int i = 0; i < N; ++i) c += w.J()[i * LDJ + l] * w.F()[i];
+            if (l < N) c = dot_batched<4>(w.J() + l, LDJ, w.F(), 1, N);
             if (useT) {
-                if (l < q) for (int a2 = 0; a2 <= l; ++a2) wv += w.T()[a2 * LDJ + l] * w.Vb()[a2];
+                if (l < q) wv = dot_range<4>(w.T() + l, LDJ, w.Vb(), 1, 0, l + 1);
             } else {                                 // long horizons: R' wv = bc by forward substitution
                 double acc = (l < q) ? w.Vb()[l] : 0.0;
                 for (int k2 = 0; k2 < q; ++k2) {
@@ -1201,7 +1290,7 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
             double v = 0.0, u = 0.0;
             if (l < N) for (int k2 = 0; k2 < N; ++k2) v += w.J()[l * LDJ + k2] * (w.dr()[k2] - w.d()[k2]);
             if (useT) {
-                if (l < q) for (int b = l; b < q; ++b) u += w.T()[l * LDJ + b] * w.np()[b];
+                if (l < q) u = dot_range<4>(w.T() + l * LDJ, 1, w.np(), 1, l, q);
             } else {                                 // R u = wv + c1 by back substitution
                 double acc = (l < q) ? w.np()[l] : 0.0;
                 for (int b = q - 1; b >= 0; --b) {
@@ -1267,7 +1356,7 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
             if (ej >= 0) {
                 if (l < N) dl = esg * w.J()[ej * LDJ + l];
             } else if (l < N) {
-                for (int i = 0; i < N; ++i) dl += w.J()[i * LDJ + l] * w.np()[i];
+                dl = dot_batched<4>(w.J() + l, LDJ, w.np(), 1, N);
             }
             // d split at q: d2 = d[q:N] (w.d) and d1 = d[0:q] (w.dr), zero elsewhere, so
             // both matvecs run full fixed-length rows (unrolled, loads batched)
@@ -1276,12 +1365,8 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
             // z = J2 d2 (primal direction) and r = T d1 = R^{-1} d1 (negative dual direction)
             double zl = 0.0, rl = 0.0;
             if (l < N) {
-#pragma unroll 4
-                for (int k2 = 0; k2 < N; ++k2) zl += w.J()[l * LDJ + k2] * w.d()[k2];
-                if (useT) {
-#pragma unroll 4
-                    for (int b = 0; b < N; ++b) rl += w.T()[l * LDJ + b] * w.dr()[b];
-                }
+                zl = dot_batched<4>(w.J() + l * LDJ, 1, w.d(), 1, N);
+                if (useT) rl = dot_batched<4>(w.T() + l * LDJ, 1, w.dr(), 1, N);
             }
             if (!useT) {                       // long horizons: back substitution on R
                 double acc = (l < q) ? dl : 0.0;
@@ -1326,10 +1411,9 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
                         double vtv = gsum<P>(vl * vl);
                         NTM_WSYNC();
                         if (l < N) {
-                            double dot = 0.0;
-                            for (int k2 = 0; k2 < N; ++k2) dot += w.J()[l * LDJ + k2] * w.hv()[k2];
-                            double f = 2.0 * dot / vtv;
-                            for (int k2 = q; k2 < N; ++k2) w.J()[l * LDJ + k2] -= f * w.hv()[k2];
+                            const double dot = dot_batched<4>(w.J() + l * LDJ, 1, w.hv(), 1, N);
+                            const double f = 2.0 * dot / vtv;
+                            axpy_sub<4>(w.J() + l * LDJ, w.hv(), f, q, N);
                         }
                     }
                     // R gains column q = [d1; h]; T = R^{-1} gains column q = [-r/h; 1/h]
@@ -1418,7 +1502,7 @@ __device__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, i
 //   from Gsave (a copy taken before the GI factorisation, dense rows).
 // ---------------------------------------------------------------------------
 template <int P, class Rows, class W>
-__device__ bool polish_phase(const Prob& pb, const W& w, const Rows* rows, int q, int l,
+__device__ __forceinline__ bool polish_phase(const Prob& pb, const W& w, const Rows* rows, int q, int l,
                              const double* Gsave, bool g_in_R, bool verify_only, int* ns_out) {
     const int N = w.n(), LD = w.ldj(), LDJ = w.ldj();
     const double Vgi = (l < N) ? w.V()[l] : 0.0;
@@ -1622,7 +1706,7 @@ __device__ bool polish_phase(const Prob& pb, const W& w, const Rows* rows, int q
 // when !verify_only (then GI's V is kept); returns success.
 // ---------------------------------------------------------------------------
 template <int P, class W>
-__device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows, int q, int l, bool verify_only,
+__device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows, int q, int l, bool verify_only,
                                int* ns_out, int* fail_kind = nullptr, int* fail_pos = nullptr,
                                double* v_out = nullptr) {
     const int N = w.n(), LD = w.ldj(), LDJ = w.ldj();
@@ -1649,24 +1733,14 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
             ssign = (kind == 4) ? 1.0 : -1.0;
         } else {                                          // state row r = j: Lin = -+Gamma_r
             const double sg = (kind == 2) ? -1.0 : 1.0;
-            const int jm = j >> 1;
-            int nnz = 0, jj = -1;
-            // fixed trip count; gt(j, c) for c > j/2 still reads inside Gt (see check)
-            constexpr int CH = 4;
-            for (int c0 = 0; c0 < N; c0 += CH) {          // batched loads
-                double g[CH];
-#pragma unroll
-                for (int u = 0; u < CH; ++u) g[u] = (c0 + u < N) ? w.gt(j, c0 + u) : 0.0;
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int u = 0; u < CH; ++u)
-                    if (c0 + u <= jm && g[u] != 0.0) { ++nnz; jj = c0 + u; }
-            }
+            const int info = w.rinfo()[j];                 // scaling pass: last non-zero column
+            const int jj = (info & (kRowMulti - 1)) - 1;
+            const int nnz = (info & kRowMulti) ? 2 : (jj >= 0 ? 1 : 0);
             if (nnz == 1) {
                 double lv = sg * w.gt(j, jj);
                 fixj = jj;
                 ufix = rows.bval(w, id) / lv;
-                nfix = -((lv * w.D()[jj]) / w.rn()[j]);
+                nfix = -((lv * w.D()[jj]) * w.irn()[j]);
             } else {
                 isgen = 1;
                 srow = j;
@@ -1674,6 +1748,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
             }
         }
     }
+    NTM_ACC(ST_C_A, tp);
     const int lane = threadIdx.x & 63;
     const unsigned long long gmask = (P == 64) ? ~0ull : (((1ull << P) - 1ull) << (lane & ~(P - 1)));
     const unsigned long long below = (1ull << lane) - 1ull;
@@ -1711,12 +1786,14 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
     // --- y_B = Gamma U_B (fixed variables only; scratch in w.Phi(), dead until the
     //     next lift) and z = y_B + e - r (scratch in w.xp(), rewritten by the rollout) ---
     NTM_WSYNC();
+    NTM_ACC(ST_C_B, tp);
     for (int r = l; r < 2 * N; r += P) {
         const double y = gamma_row_dot<4>(w, r, w.dr());
         w.Phi()[r] = y;
         w.xp()[r] = y + w.e()[r] - ((r & 1) ? pb.r[1] : pb.r[0]);
     }
     NTM_WSYNC();
+    NTM_ACC(ST_C_Y, tp);
     // --- square, triangular E (nS == nF, the common "boundary arc": the state held
     //     at its bound by every free input).  The active general rows then pin the
     //     free variables down on their own: sorted by their last free variable they
@@ -1736,10 +1813,9 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
             if (r >= 2 * N) {                                  // rate row of input i: e_i - e_{i-1}
                 const int i = r - 2 * N;
                 lj = ((fm >> i) & 1ull) ? i : (((fm >> (i - 1)) & 1ull) ? i - 1 : -1);
-            } else {                                           // state row r: Gamma_r, columns j <= r/2
-                const int jm = r >> 1;
-                for (int j = 0; j < N; ++j)
-                    if (j <= jm && ((fm >> j) & 1ull) && w.gt(r, j) != 0.0) lj = j;
+            } else {                                           // state row r: from its last non-zero
+                lj = (w.rinfo()[r] & (kRowMulti - 1)) - 1;     // column down to the first free one
+                while (lj >= 0 && !(((fm >> lj) & 1ull) && w.gt(r, lj) != 0.0)) --lj;
             }
             if (lj >= 0) lastf = __popcll(fm & ((1ull << lj) - 1ull));
             perm[l] = -1;
@@ -1749,7 +1825,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
         NTM_WSYNC();
         sq = gmaxi<P>((l < nS && perm[l] < 0) ? 1 : 0) == 0;
     }
-    NTM_ACC(ST_P_CLASS, tp);
+    NTM_ACC(ST_C_SQ, tp);
     // --- g_F (lane a = compact index) ---
     double gl = 0.0;
     if (!sq && l < nF) {
@@ -2106,9 +2182,11 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
         // y = Gamma U once, for the primal check (state rows) and the gradient
         for (int r = l; r < 2 * N; r += P) w.xp()[r] = gamma_row_dot<4>(w, r, w.U());
         NTM_WSYNC();
+        NTM_ACC(ST_K_Y, tp);
         double vmax = gmax<P>(l < N ? fabs(vfin) : 0.0);
         Pick vf = rows.template check<P>(w, vfin, l, true, fmax(1.0, vmax), w.xp());
         ok = vf.p == 0;
+        NTM_ACC(ST_K_CHK, tp);
         // gradient G~V + F~ = D (2 Gamma' Om y) + F~
         double res = 0.0;
         if (l < N) {
@@ -2116,6 +2194,7 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
             const double g2 = qdot_rows<4>(cl, w.xp(), N, l, q00, q01, q10, q11);   // terms i < l masked
             res = w.D()[l] * (2 * g2) + w.F()[l];
         }
+        NTM_ACC(ST_K_GRAD, tp);
         if (sq) {
             // square path: the multipliers from E' mu = grad_F (E upper triangular in
             // sorted order), back substitution; lane t owns row t and grad at f_t
@@ -2131,9 +2210,26 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
             if (l < nS) w.np()[perm[l]] = mu;
             NTM_WSYNC();
         }
-        if (l < N) {
-            for (int s2 = 0; s2 < nS; ++s2) res -= w.np()[s2] * gen_n(s2, l);
+        NTM_ACC(ST_K_MU, tp);
+        // - sum_s mu_s n_s[l]: for state rows n_s[l] = -ssg_s Gamma_{r_s l} D_l irn_{r_s},
+        // i.e. + D_l (Gamma' z)_l with z_{r_s} = mu_s ssg_s irn_{r_s} (zero on the other
+        // rows; scratch in w.Phi(), dead until the next lift); rate rows directly
+        double* const z = w.Phi();
+        for (int r = l; r < 2 * N; r += P) z[r] = 0.0;
+        NTM_WSYNC();
+        if (l < nS) {
+            const int r = w.srw()[l];
+            if (r < 2 * N) z[r] = (w.np()[l] * w.ssg()[l]) * w.irn()[r];
         }
+        NTM_WSYNC();
+        if (l < N) {
+            const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;
+            res += w.D()[l] * qdot_rows<4>(cl, z, N, l, 1.0, 0.0, 0.0, 1.0);   // terms i < l masked
+            if (rows.has_rate())
+                for (int s2 = 0; s2 < nS; ++s2)
+                    if (w.srw()[s2] >= 2 * N) res -= w.np()[s2] * gen_n(s2, l);
+        }
+        NTM_ACC(ST_K_SUB, tp);
         // multipliers: general row s on lane s, fixed variable j on lane j; each
         // lane keeps its most negative one and that row's active-list position
         double mval = 0.0;
@@ -2176,20 +2272,37 @@ __device__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows
 // Returns (group-uniform) whether sum|Uold - U| < eps; updates Uold.
 // ---------------------------------------------------------------------------
 template <int P, class W>
-__device__ bool rollout_phase(const Prob& pb, const W& w, double x0, double x1, int l) {
+__device__ __forceinline__ bool rollout_phase(const Prob& pb, const W& w, double x0, double x1, int l) {
     const int N = w.n();
     const Coef& k = pb.k;
     if (l == 0) {
         double y0 = x0, y1 = x1;
         w.xp()[0] = y0;
         w.xp()[1] = y1;
-        for (int i = 0; i < N; ++i) {
-            double n0 = (w.a11()[i] * y0 + w.bb()[i] * w.U()[i]) + k.C1;
-            double n1 = (w.a21()[i] * y0 + k.a22 * y1) + k.C2;
-            y0 = n0;
-            y1 = n1;
-            w.xp()[2 * i + 2] = y0;
-            w.xp()[2 * i + 3] = y1;
+        constexpr int CH = 4;                   // the loads of CH steps ahead of their stores
+        for (int i0 = 0; i0 < N; i0 += CH) {
+            double ca[CH], cb[CH], cc[CH], cu[CH];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int i = i0 + u;
+                ca[u] = i < N ? w.a11()[i] : 0.0;
+                cb[u] = i < N ? w.bb()[i] : 0.0;
+                cc[u] = i < N ? w.a21()[i] : 0.0;
+                cu[u] = i < N ? w.U()[i] : 0.0;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int i = i0 + u;
+                if (i < N) {
+                    const double n0 = (ca[u] * y0 + cb[u] * cu[u]) + k.C1;
+                    const double n1 = (cc[u] * y0 + k.a22 * y1) + k.C2;
+                    y0 = n0;
+                    y1 = n1;
+                    w.xp()[2 * i + 2] = y0;
+                    w.xp()[2 * i + 3] = y1;
+                }
+            }
         }
     }
     NTM_WSYNC();
@@ -2235,7 +2348,7 @@ __device__ __forceinline__ void plant_step(const Prob& pb, double x0, double x1,
 // exactly and KKT-certified.
 // ---------------------------------------------------------------------------
 template <int P, class W>
-__device__ int shifted_into_act(const Prob& pb, const W& w, const int* c, int l) {
+__device__ __forceinline__ int shifted_into_act(const Prob& pb, const W& w, const int* c, int l) {
     const int N = w.n();
     const int lane = threadIdx.x & 63;
     const unsigned long long gmask = (P == 64) ? ~0ull : (((1ull << P) - 1ull) << (lane & ~(P - 1)));
@@ -2275,7 +2388,7 @@ __device__ int shifted_into_act(const Prob& pb, const W& w, const int* c, int l)
 // one inner iteration's QP: build -> scale -> GI -> polish -> w.U()
 // ---------------------------------------------------------------------------
 template <int P, class W>
-__device__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l, int* qp_iters,
+__device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l, int* qp_iters,
                         int* q_out, int* ns_out, int slot, int* n_try = nullptr, int* n_girun = nullptr,
                         int it = 0) {
     const int N = w.n();

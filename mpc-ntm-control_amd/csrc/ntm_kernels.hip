@@ -68,7 +68,7 @@ __device__ __forceinline__ int64_t xcd_swizzle(int64_t b, int64_t nb) {
 // comes from the caller, so each slot is validated before use: count in
 // [0, N], ids in [0, rows), no repeats; anything else disables the slot.
 template <int P, class W>
-__device__ void load_candidates(const Prob& pb, const W& w, int64_t B, int64_t s, const int32_t* ws, int l) {
+__device__ __forceinline__ void load_candidates(const Prob& pb, const W& w, int64_t B, int64_t s, const int32_t* ws, int l) {
     const int N = w.n();
     const int nrows = StructRows(pb).rows();
     const int32_t* wss = ws + s * (2 * (N + 1));
