@@ -1802,9 +1802,12 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     //     by back substitution in the certificate; no Gram of the free columns and
     //     no bordered elimination.  perm[t] = the general row whose last free
     //     variable is the t-th (scratch ints in the R block; E goes to the J block).
-    int* const perm = reinterpret_cast<int*>(w.R());
-    bool sq = false;
-    if (nS == nF && nS > 0 && !collide) {
+    int* const perm = reinterpret_cast<int*>(w.R());      // sorted row t -> general row
+    int* const colrow = perm + (N + 1);                    // compact column -> row ending there
+    bool sq = false;                                       // echelon path (k = nF - nS <= 1)
+    int nc = -1;                                           // k = 1: the non-pivot compact column
+    const int kdim = nF - nS;
+    if ((kdim == 1 || (kdim == 0 && nS > 0)) && !collide) {
         const unsigned long long fm = bal >> (lane & ~(P - 1));   // bit j: variable j is free
         int lastf = -1;
         if (l < nS) {
@@ -1818,12 +1821,18 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 while (lj >= 0 && !(((fm >> lj) & 1ull) && w.gt(r, lj) != 0.0)) --lj;
             }
             if (lj >= 0) lastf = __popcll(fm & ((1ull << lj) - 1ull));
-            perm[l] = -1;
         }
+        if (l < nF) colrow[l] = -1;
         NTM_WSYNC();
-        if (lastf >= 0) perm[lastf] = l;                       // a repeated last column leaves a hole
+        if (lastf >= 0) colrow[lastf] = l;                     // a repeated last column leaves a hole
         NTM_WSYNC();
-        sq = gmaxi<P>((l < nS && perm[l] < 0) ? 1 : 0) == 0;
+        const unsigned long long holes = __ballot(l < nF && colrow[l] < 0) & gmask;
+        if ((int)__popcll(holes) == kdim) {                    // every row ends in its own column
+            sq = true;
+            nc = kdim ? uni<P>((int)__ffsll((long long)(holes >> (lane & ~(P - 1)))) - 1) : -1;
+            if (l < nS) perm[l] = colrow[l + ((nc >= 0 && l >= nc) ? 1 : 0)];
+            NTM_WSYNC();
+        }
     }
     NTM_ACC(ST_C_SQ, tp);
     // --- g_F (lane a = compact index) ---
@@ -1902,20 +1911,29 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     bool ok = !collide;
     int fk = ok ? 0 : 3, fpos_out = 0;
     double vfin = 0.0;
-    double sq_id = 0.0;                                   // square path: 1 / E[t][t] on lane t
+    double sq_id = 0.0;                                   // echelon path: 1 / E_p[t][t] on lane t
+    bool y_ready = false;                                 // k = 1: y = Gamma U already in w.xp()
     if (sq) {
-        // sorted E (row t = general row perm[t], n x n, row-major at Lp[t LD + a]) and h
+        // Sorted E over the pivot columns (row t = general row perm[t] ends in pivot
+        // column pc(t) = t + (t >= nc); lower triangular, n x n row-major at Lp[t LD + u]),
+        // the non-pivot column e_c (k = 1) and h
         const int n = nS;
+        auto pc = [&](int u) { return u + ((nc >= 0 && u >= nc) ? 1 : 0); };
         for (int idx = l; idx < n * n; idx += P) {
-            const int t = idx / n, a = idx - t * n;
-            Lp[t * LD + a] = (a <= t) ? gen_n(perm[t], w.fidx()[a]) : 0.0;
+            const int t = idx / n, u = idx - t * n;
+            Lp[t * LD + u] = (u <= t) ? gen_n(perm[t], w.fidx()[pc(u)]) : 0.0;
         }
-        double acc = (l < n) ? hs_of(perm[l]) : 0.0;
+        double acc = 0.0, acz = 0.0;
+        if (l < n) {
+            acc = hs_of(perm[l]);
+            if (nc >= 0 && nc < pc(l)) acz = -gen_n(perm[l], w.fidx()[nc]);
+        }
         NTM_WSYNC();
         if (l < n) sq_id = 1.0 / Lp[l * LD + l];
         NTM_ACC(ST_S_E, tp);
-        // E V_F = h: lane t owns row t; step t broadcasts x_t and updates the rows below
-        double x = 0.0;
+        // E_p V_p = h and (k = 1) E_p Z_p = -e_c: lane t owns row t; step t broadcasts
+        // x_t (z_t) and updates the rows below
+        double x = 0.0, zz = 0.0;
         double en = (l > 0 && l < n) ? Lp[l * LD] : 0.0;      // E[l][t], loaded one step ahead
         for (int t = 0; t < n; ++t) {
             const double et = en;
@@ -1923,13 +1941,54 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             const double xt = gbcast<P>(acc * sq_id, t);
             if (l == t) x = xt;
             acc -= et * xt;
+            if (nc >= 0) {
+                const double zt = gbcast<P>(acz * sq_id, t);
+                if (l == t) zz = zt;
+                acz -= et * zt;
+            }
         }
-        ok = gmaxi<P>((l < n && !isfinite(x)) ? 1 : 0) == 0;
+        ok = gmaxi<P>((l < n && !(isfinite(x) && isfinite(zz))) ? 1 : 0) == 0;
+        // V_0 (pivots from E_p V_p = h, fixed values, 0 on the non-pivot column) and Z
+        const int rk = (fpos == nc) ? 0 : fpos - ((nc >= 0 && fpos > nc) ? 1 : 0);
+        const double xs = __shfl(x, (l < N && !fixed) ? rk : 0, P);
+        const double zs = __shfl(zz, (l < N && !fixed) ? rk : 0, P);
+        const double v0 = fixed ? vb : ((fpos == nc) ? 0.0 : xs);
+        vfin = v0;
+        if (ok && nc >= 0) {
+            // k = 1: the minimum along V_0 + w Z, Z = e_c + Z_p:
+            //   w = -(2 yz' Om (y0 + e - r)) / (2 yz' Om yz), y0 = Gamma D V_0, yz = Gamma D Z
+            const double zv = fixed ? 0.0 : ((fpos == nc) ? 1.0 : zs);
+            if (l < N) {
+                w.U()[l] = w.D()[l] * v0;
+                w.d()[l] = w.D()[l] * zv;
+            }
+            NTM_WSYNC();
+            for (int r = l; r < 2 * N; r += P) {
+                w.xp()[r] = gamma_row_dot<4>(w, r, w.U());
+                w.Phi()[r] = gamma_row_dot<4>(w, r, w.d());      // scratch (hs_of is done with it)
+            }
+            NTM_WSYNC();
+            double num = 0.0, den = 0.0;
+            if (l < N) {
+                const double y0a = w.xp()[2 * l] + w.e()[2 * l] - pb.r[0];
+                const double y0b = w.xp()[2 * l + 1] + w.e()[2 * l + 1] - pb.r[1];
+                const double za = w.Phi()[2 * l], zb = w.Phi()[2 * l + 1];
+                const double oa = q00 * za + q01 * zb, ob = q10 * za + q11 * zb;
+                num = oa * y0a + ob * y0b;
+                den = oa * za + ob * zb;
+            }
+            num = gsum<P>(num);
+            den = gsum<P>(den);
+            ok = den > 0.0 && den < kInf && isfinite(num);
+            const double wv = ok ? -(num / den) : 0.0;
+            vfin = v0 + wv * zv;
+            for (int r = l; r < 2 * N; r += P) w.xp()[r] += wv * w.Phi()[r];   // y = y0 + w yz
+            y_ready = true;
+        }
         if (!ok) fk = 3;
-        const double vsc = __shfl(x, (l < N && !fixed) ? fpos : 0, P);
-        vfin = fixed ? vb : vsc;
         NTM_ACC(ST_S_Y, tp);
     } else if (fused) {
+        // E rows over the free variables (one entry per lane) and h; the trailing    } else if (fused) {
         // E rows over the free variables (one entry per lane) and h; the trailing
         // block of A is zero and is never stored (the elimination starts it at 0)
         for (int idx = l; idx < nF * nS; idx += P) {
@@ -2180,8 +2239,10 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         if (l < N) { w.V()[l] = vfin; w.U()[l] = w.D()[l] * vfin; }
         NTM_WSYNC();
         // y = Gamma U once, for the primal check (state rows) and the gradient
-        for (int r = l; r < 2 * N; r += P) w.xp()[r] = gamma_row_dot<4>(w, r, w.U());
-        NTM_WSYNC();
+        if (!y_ready) {
+            for (int r = l; r < 2 * N; r += P) w.xp()[r] = gamma_row_dot<4>(w, r, w.U());
+            NTM_WSYNC();
+        }
         NTM_ACC(ST_K_Y, tp);
         double vmax = gmax<P>(l < N ? fabs(vfin) : 0.0);
         Pick vf = rows.template check<P>(w, vfin, l, true, fmax(1.0, vmax), w.xp());
@@ -2200,7 +2261,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             // sorted order), back substitution; lane t owns row t and grad at f_t
             if (l < N && !fixed) w.d()[fpos] = res;
             NTM_WSYNC();
-            double acc = (l < nS) ? w.d()[l] : 0.0, mu = 0.0;
+            double acc = (l < nS) ? w.d()[l + ((nc >= 0 && l >= nc) ? 1 : 0)] : 0.0, mu = 0.0;
             for (int u = nS - 1; u >= 0; --u) {
                 const double eu = (l < u) ? Lp[u * LD + l] : 0.0;
                 const double mu_u = gbcast<P>(acc * sq_id, u);
