@@ -2529,11 +2529,37 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                         NTM_WSYNC();
                         if (pk.p < 0) {
                             stop = true;
-                        } else if (cq < N && fk == 2) {
-                            if (l == 0) w.act()[cq] = pk.p;
-                            ++cq;
-                        } else if (l == 0) {               // a negative multiplier too (fk 4), or a full
-                            w.act()[fp] = pk.p;            // set: it swaps out the smallest multiplier
+                        } else {
+                            // A state or rate row whose last variable is held by a bound row
+                            // takes that bound row's place (adding it next to the bound would
+                            // leave it no free variable: a singular system).  This is how a
+                            // boundary arc moves by one stage from step to step.  With a
+                            // negative multiplier too (fk 4) that row goes as well.
+                            int kind, jr, jl = -1;
+                            rows.decode(pk.p, N, kind, jr);
+                            if ((kind == 2 || kind == 3) && jr >= 0) jl = (w.rinfo()[jr] & (kRowMulti - 1)) - 1;
+                            else if (kind >= 4) jl = jr;
+                            int my = -1;
+                            bool drop_me = false;
+                            if (l < cq) {
+                                my = w.act()[l];
+                                int k2, j2;
+                                rows.decode(my, N, k2, j2);
+                                drop_me = (jl >= 0 && k2 < 2 && j2 == jl) || (fk == 4 && l == fp);
+                            }
+                            const int lane = threadIdx.x & 63;
+                            const unsigned long long gm =
+                                (P == 64) ? ~0ull : (((1ull << P) - 1ull) << (lane & ~(P - 1)));
+                            const unsigned long long keepm = __ballot(l < cq && !drop_me) & gm;
+                            const int nkeep = uni<P>((int)__popcll(keepm));
+                            NTM_WSYNC();
+                            if (nkeep < N) {
+                                if (l < cq && !drop_me) w.act()[__popcll(keepm & ((1ull << lane) - 1ull))] = my;
+                                if (l == 0) w.act()[nkeep] = pk.p;
+                                cq = nkeep + 1;
+                            } else if (l == 0) {           // a full set: swap out the smallest multiplier
+                                w.act()[fp] = pk.p;
+                            }
                         }
                     } else if (!stop) {                    // dual: drop position fp
                         int an = 0;
