@@ -5,6 +5,6 @@ set -o pipefail
 mkdir -p gpurun_out
 bash tools/gpu_cmd.sh || exit $?
 timeout -k 10 300 python bench.py --steps 5 --warmup 1 > gpurun_out/bench_cpu.json 2> gpurun_out/bench_cpu.err || exit $?
-TAG=r01 bash tools/prof_r01.sh > gpurun_out/prof.log 2>&1 || exit $?
-TAG=r01 bash tools/prof_pmc.sh > gpurun_out/pmc.log 2>&1 || exit $?
+TAG=${TAG:-r02} bash tools/prof_r01.sh > gpurun_out/prof.log 2>&1 || exit $?
+TAG=${TAG:-r02} bash tools/prof_pmc.sh > gpurun_out/pmc.log 2>&1 || exit $?
 bash tools/gpu_configs.sh || exit $?
