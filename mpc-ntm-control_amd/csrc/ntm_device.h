@@ -124,6 +124,12 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 constexpr int kMaxNT = 32;         // explicit R^{-1} in GI up to this horizon (WS::useT)
 constexpr int kRepairs = 8;
+// A constant row (Lin_i = 0: the x_0 rows of getWLc, state rows Gamma doesn't
+// reach) is violated when b_i < -kConstTol (D22, oracle CONST_ROW_TOL): the same
+// absolute 1e-9 the KKT certificate allows on a unit-scale row.  An exact test
+// turned a state that the plant step leaves one ulp outside a bound the
+// previous plan held it at (x_{k+1} = xmin - ulp) into an infeasible QP.
+constexpr double kConstTol = 1e-9;
 constexpr int kRowMulti = 256;     // WS::rinfo flag: the state row has two or more non-zeros        // single-row repairs of a failed warm-start candidate
 constexpr int kGiWarmRejected = 100;   // gi_solve: the warm-start set was not dual feasible (caller reruns cold)
 
@@ -922,22 +928,23 @@ struct StructRows {
         return kind < 2 ? w.D()[j] : 1.0 / w.irn()[j];
     }
 
-    // constant rows (x_0 rows; state rows with Gamma_r == 0): 0 <= b or infeasible (D15)
+    // constant rows (x_0 rows; state rows with Gamma_r == 0): 0 <= b, to kConstTol,
+    // or infeasible (D15, D22)
     template <int P, class W>
     __device__ __forceinline__ bool feasible_const(const W& w, double x0, double x1, int l) const {
         int bad = 0;
         if (has_state()) {
             if (l == 0) {
-                bad |= (x0 - xmin(0)) < 0.0;
-                bad |= (x1 - xmin(1)) < 0.0;
-                bad |= (xmax(0) - x0) < 0.0;
-                bad |= (xmax(1) - x1) < 0.0;
+                bad |= (x0 - xmin(0)) < -kConstTol;
+                bad |= (x1 - xmin(1)) < -kConstTol;
+                bad |= (xmax(0) - x0) < -kConstTol;
+                bad |= (xmax(1) - x1) < -kConstTol;
             }
             for (int r = l; r < 2 * w.n(); r += P) {
                 if (w.irn()[r] == 0.0) {
                     int c = r & 1;
-                    bad |= (w.e()[r] - xmin(c)) < 0.0;
-                    bad |= (xmax(c) - w.e()[r]) < 0.0;
+                    bad |= (w.e()[r] - xmin(c)) < -kConstTol;
+                    bad |= (xmax(c) - w.e()[r]) < -kConstTol;
                 }
             }
         }
@@ -1055,7 +1062,7 @@ struct DenseRows {
             double bi = bval(w, i);
             if (!isfinite(ss) || !isfinite(bi)) bad |= 1;
             rnrm[i] = ss > 0.0 ? sqrt(ss) : 0.0;
-            if (!(ss > 0.0) && bi < 0.0) bad |= 2;
+            if (!(ss > 0.0) && bi < -kConstTol) bad |= 2;   // constant row violated (D15, D22)
         }
         NTM_WSYNC();
         return gmaxi<P>(bad);
@@ -2273,19 +2280,39 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         }
         NTM_ACC(ST_K_MU, tp);
         // - sum_s mu_s n_s[l]: for state rows n_s[l] = -ssg_s Gamma_{r_s l} D_l irn_{r_s},
-        // i.e. + D_l (Gamma' z)_l with z_{r_s} = mu_s ssg_s irn_{r_s} (zero on the other
-        // rows; scratch in w.Phi(), dead until the next lift); rate rows directly
+        // i.e. + D_l sum_s Gamma_{r_s l} z_s with z_s = mu_s ssg_s irn_{r_s}: a sparse
+        // pass over the nS active general rows only (z_s scratch in w.Phi(), dead
+        // until the next lift; rows r_s >= 2N are rate rows, handled directly)
         double* const z = w.Phi();
-        for (int r = l; r < 2 * N; r += P) z[r] = 0.0;
-        NTM_WSYNC();
         if (l < nS) {
             const int r = w.srw()[l];
-            if (r < 2 * N) z[r] = (w.np()[l] * w.ssg()[l]) * w.irn()[r];
+            z[l] = (r < 2 * N) ? (w.np()[l] * w.ssg()[l]) * w.irn()[r] : 0.0;
         }
         NTM_WSYNC();
         if (l < N) {
-            const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;
-            res += w.D()[l] * qdot_rows<4>(cl, z, N, l, 1.0, 0.0, 0.0, 1.0);   // terms i < l masked
+            const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;   // cl[r] = gt(r, l), r >= 2l
+            double sub = 0.0;
+            constexpr int CH = 4;
+            for (int s0 = 0; s0 < nS; s0 += CH) {
+                int rr[CH];
+                double zv[CH], gv[CH];
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    const bool in = s0 + u < nS;
+                    rr[u] = in ? w.srw()[s0 + u] : 0;
+                    zv[u] = in ? z[s0 + u] : 0.0;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    const bool on = s0 + u < nS && rr[u] < 2 * N && (rr[u] >> 1) >= l;
+                    gv[u] = on ? cl[rr[u]] : 0.0;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < CH; ++u) sub += gv[u] * zv[u];
+            }
+            res += w.D()[l] * sub;
             if (rows.has_rate())
                 for (int s2 = 0; s2 < nS; ++s2)
                     if (w.srw()[s2] >= 2 * N) res -= w.np()[s2] * gen_n(s2, l);

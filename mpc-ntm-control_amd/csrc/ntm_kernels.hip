@@ -569,12 +569,18 @@ bool force_generic() {
     static bool g = std::getenv("NTM_GENERIC") != nullptr;
     return g;
 }
+#ifdef NTM_RU_ONLY20
+// resource-usage check of the N=20 hot kernel alone (make ru20): every horizon
+// goes to it; the library built this way is not for use
+#define NTM_DISPATCH_P(N, CALL) CALL(64, 20)
+#else
 #define NTM_DISPATCH_P(N, CALL)                                                     \
     (force_generic() ? (lanes_for(N) == 16 ? CALL(16, 0) : (lanes_for(N) == 32 ? CALL(32, 0) : CALL(64, 0))) \
     : lanes_for(N) == 16 ? ((N) == 10 ? CALL(16, 10) : CALL(16, 0))                  \
                         : (lanes_for(N) == 32 ? CALL(32, 0)                          \
                                               : ((N) == 20 ? CALL(64, 20)            \
                                                            : ((N) == 50 ? CALL(64, 50) : CALL(64, 0)))))
+#endif
 
 struct DevBuf {
     ntm_ctx* ctx;

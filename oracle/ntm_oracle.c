@@ -32,6 +32,8 @@
 
 #define NMAX NTM_MAX_N
 #define MMAX (8 * NMAX + 4)   /* getWLc rows + rate rows (NTM_MODE_FULL_DU) */
+/* constant-row violation tolerance (D22; oracle/ntm_oracle.py CONST_ROW_TOL) */
+#define CONST_ROW_TOL 1e-9
 
 typedef struct {
     double a11c, a21num_den, a22, bc, C1, C2, wmarg2, wdep;
@@ -228,7 +230,7 @@ static int orc_gi(int n, int m, const double* G, const double* F, const double* 
         for (int j = 0; j < n; ++j) s += Lin[(size_t)j * m + i] * Lin[(size_t)j * m + i];
         nrm[i] = sqrt(s);
         nz[i] = s > 0.0;
-        if (!nz[i] && -b[i] > 0.0) return NTM_EXIT_INFEASIBLE;
+        if (!nz[i] && -b[i] > CONST_ROW_TOL) return NTM_EXIT_INFEASIBLE;   /* D15, D22 */
     }
     /* Cholesky G = Lc Lc' (lower, row-major Lc[i*n+j]) */
     for (int j = 0; j < n; ++j) {

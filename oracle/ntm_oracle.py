@@ -304,6 +304,10 @@ def rate_rows(N):
 
 EXIT_OK, EXIT_MAXIT, EXIT_INFEASIBLE, EXIT_NONFINITE = 1, 0, -2, -7
 GI_DEP_TOL = 1e-8
+# A constant row (Lin_i == 0) is violated when b_i < -CONST_ROW_TOL (DESIGN.md
+# D22): quadprog judges feasibility to a tolerance, and the closed loop's plant
+# step can leave x_{k+1} one ulp outside a bound the plan held it at.
+CONST_ROW_TOL = 1e-9
 
 
 def _givens(a, b):
@@ -320,7 +324,8 @@ def qp_dual_active_set(G, F, Lin, b, max_iter=None):
     This is the oracle's stand-in for MathWorks ``quadprog`` (NTM_MPC_Sim.m:97),
     which is closed source and absent.  Returns (U, exitflag, active_rows,
     multipliers, iterations).  Constant rows (Lin_i == 0, e.g. the x_0 rows of
-    getWLc) are checked directly: 0 <= b_i or the problem is infeasible (D15).
+    getWLc) are checked directly: 0 <= b_i (to CONST_ROW_TOL) or the problem is
+    infeasible (D15, D22).
     """
     n = G.shape[0]
     m = Lin.shape[0]
@@ -333,7 +338,7 @@ def qp_dual_active_set(G, F, Lin, b, max_iter=None):
     Nc = -Lin
     bc = -b
     nonzero = np.any(Nc != 0.0, axis=1)
-    if np.any((~nonzero) & (bc > 0.0)):          # 0 >= bc violated  -> infeasible (D15)
+    if np.any((~nonzero) & (bc > CONST_ROW_TOL)):   # 0 >= bc violated  -> infeasible (D15, D22)
         return np.zeros(n), EXIT_INFEASIBLE, [], np.zeros(0), 0
     nrm = np.linalg.norm(Nc, axis=1)
     try:
@@ -348,12 +353,13 @@ def qp_dual_active_set(G, F, Lin, b, max_iter=None):
     it = 0
     while True:
         s = Nc @ U - bc
-        viol = np.where(nonzero, s / np.where(nrm > 0, nrm, 1.0), 0.0)
+        # constant rows were checked above (never candidates), active rows are held
+        viol = np.where(nonzero, s / np.where(nrm > 0, nrm, 1.0), np.inf)
         if act:
-            viol[act] = 0.0
+            viol[act] = np.inf
         p = int(np.argmin(viol))
         # stop when the worst row is satisfied to 1e-12 of its own scale
-        if s[p] >= -1e-12 * max(nrm[p] * np.max(np.abs(U), initial=1.0), abs(bc[p])):
+        if viol[p] == np.inf or s[p] >= -1e-12 * max(nrm[p] * np.max(np.abs(U), initial=1.0), abs(bc[p])):
             return U, EXIT_OK, act, u, it
         up = np.append(u, 0.0)
         while True:

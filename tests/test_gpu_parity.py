@@ -344,6 +344,20 @@ def test_step_reference_x0_infeasible(ctl):
     assert (H(out["U"]) == 0).all()
 
 
+def test_quadprog_constant_row_tolerance(ctl):
+    """D22: a constant row (Lin_i = 0) is violated only beyond 1e-9, as in both
+    oracles (tests/test_oracle.py::test_constant_row_tolerance)."""
+    bs = [-7e-18, -0.9e-9, -1e-6]
+    B = len(bs)
+    G = np.tile(np.eye(3).reshape(9, 1), (1, B))
+    F = np.tile(np.array([1.0, -2.0, 0.5])[:, None], (1, B))
+    Lin = np.tile(np.array([[0.0, 0.0, 0.0], [1.0, 0.0, 0.0]]).reshape(-1, order="F")[:, None], (1, B))
+    b = np.array([[b0, 10.0] for b0 in bs]).T
+    U, flag, _ = ctl.quadprog(T(G), T(F), T(Lin), T(b))
+    np.testing.assert_array_equal(H(flag), [1, 1, -2])
+    np.testing.assert_allclose(H(U)[:, :2], -F[:, :2], atol=1e-15)
+
+
 def test_step_nonfinite_flag(ctl):
     N = 20
     cfg, ocfg = cfgs(N, 2)

@@ -13,6 +13,7 @@ from pathlib import Path
 import numpy as np
 import pytest
 
+from oracle import cbind
 from oracle import ntm_oracle as O
 
 GOLD = Path(__file__).resolve().parent / "golden"
@@ -145,6 +146,22 @@ def test_reference_x0_is_infeasible():
     assert flag == O.EXIT_INFEASIBLE and np.all(U == 0)
     st = O.mpc_step(x0, Rho, np.full(3, np.inf), PH, c)
     assert st["exitflag"] == -2 and st["u"] == 0
+
+
+def test_constant_row_tolerance():
+    """D22: a constant row (Lin_i = 0) is violated only beyond CONST_ROW_TOL = 1e-9,
+    as quadprog judges feasibility to a tolerance (the plant step can leave x_{k+1}
+    one ulp outside a bound the plan held it at).  Both oracles agree."""
+    G, F = np.eye(3), np.array([1.0, -2.0, 0.5])
+    Lin = np.array([[0.0, 0.0, 0.0], [1.0, 0.0, 0.0]])
+    for b0, flag in ((-7e-18, O.EXIT_OK), (-0.9e-9, O.EXIT_OK), (-1e-6, O.EXIT_INFEASIBLE)):
+        b = np.array([b0, 10.0])
+        U, fl, _ = O.qp_solve(G, F, Lin, b)
+        Uc, flc, _ = cbind.qp(G, F, Lin, b)
+        assert fl == flag and flc == flag
+        if flag == O.EXIT_OK:
+            np.testing.assert_allclose(U, -F, atol=1e-15)
+            np.testing.assert_allclose(Uc, -F, atol=1e-15)
 
 
 # ------------------------------------------------------------------ QP
