@@ -1723,7 +1723,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     // --- classify active rows: single-entry rows fix a variable, the rest are general ---
     if (l < N) w.fx()[l] = 0;
     NTM_WSYNC();
-    int isgen = 0, fixj = -1, id = -1, srow = 0;
+    int isgen = 0, fixj = -1, id = -1, srow = 0, constrow = 0;
     double ufix = 0.0, nfix = 0.0, ssign = 0.0;
     if (l < q) {
         id = w.act()[l];
@@ -1740,10 +1740,15 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             ssign = (kind == 4) ? 1.0 : -1.0;
         } else {                                          // state row r = j: Lin = -+Gamma_r
             const double sg = (kind == 2) ? -1.0 : 1.0;
-            const int info = w.rinfo()[j];                 // scaling pass: last non-zero column
+            // an x_0 row (j < 0) or a state row Gamma doesn't reach has Lin = 0: a
+            // constant row is never active (a caller's or a shifted candidate can
+            // hold one); the set is rejected like a colliding one
+            const int info = (j >= 0) ? w.rinfo()[j] : 0;  // scaling pass: last non-zero column
             const int jj = (info & (kRowMulti - 1)) - 1;
             const int nnz = (info & kRowMulti) ? 2 : (jj >= 0 ? 1 : 0);
-            if (nnz == 1) {
+            if (nnz == 0) {
+                constrow = 1;
+            } else if (nnz == 1) {
                 double lv = sg * w.gt(j, jj);
                 fixj = jj;
                 ufix = rows.bval(w, id) / lv;
@@ -1768,7 +1773,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             w.sidx()[k] = l;                              // its position in the active list
             w.srw()[k] = srow;
             w.ssg()[k] = ssign;
-        } else {
+        } else if (!constrow) {
             w.fx()[fixj] = (unsigned char)(l + 1);       // tagged by the writing lane
             w.Uf()[fixj] = ufix;
             w.hv()[fixj] = nfix;
@@ -1776,8 +1781,10 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     }
     NTM_WSYNC();
     // two active rows fixing one variable (only a caller-supplied candidate can
-    // do that; GI never adds a dependent row) cannot be certified: reject
-    const bool collide = gmaxi<P>((l < q && !isgen && w.fx()[fixj] != (unsigned char)(l + 1)) ? 1 : 0) != 0;
+    // do that; GI never adds a dependent row) cannot be certified: reject; so is a
+    // set holding a constant row
+    const bool collide =
+        gmaxi<P>((l < q && !isgen && (constrow || w.fx()[fixj] != (unsigned char)(l + 1))) ? 1 : 0) != 0;
     const bool fixed = (l < N) && w.fx()[l];
     const double uf = fixed ? w.Uf()[l] : 0.0;
     const double vb = fixed ? uf / w.D()[l] : 0.0;
@@ -2458,8 +2465,8 @@ __device__ __forceinline__ int shifted_into_act(const Prob& pb, const W& w, cons
             dup = id;
         } else {
             const int blk = id / 6, rr = id - 6 * blk;
-            if (blk >= 1) nid = id - 6;
-            if (blk == N - 1 && rr < 2) dup = id;
+            if (blk >= 2 || (blk == 1 && rr < 2)) nid = id - 6;   // x_1's state rows would become
+            if (blk == N - 1 && rr < 2) dup = id;                  // x_0 rows (constant): dropped
         }
     }
     const unsigned long long bk = __ballot(nid >= 0) & gmask;

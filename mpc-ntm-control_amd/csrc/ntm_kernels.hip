@@ -150,6 +150,13 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, 
     NTM_TRACE_SET(s, g, l);
     if (s >= B) return;
     auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
+#ifdef NTM_POISON
+    // debug build (make poison): the workspace starts as NTM_POISON-valued doubles, so
+    // a read of LDS this launch never wrote shows up as a run-to-run difference
+    // (tools/determinism.py + compare_runs.py; this found the x_0-row read of rinfo[-1])
+    for (int e = l; e < ws_bytes(N) / 8; e += P) w.base[e] = NTM_POISON;
+    NTM_WSYNC();
+#endif
     const double x0 = x_k[2 * s], x1 = x_k[2 * s + 1];
     if (active_ws) {
         load_candidates<P>(pb, w, B, s, active_ws, l);

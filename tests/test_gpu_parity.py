@@ -462,6 +462,48 @@ def test_step_garbage_workspace_is_ignored(ctl):
     assert torch.max(torch.abs(out["U"] - ref["U"])).item() <= U_TOL * cfg.umax
 
 
+def test_step_constant_rows_in_workspace_are_rejected(ctl):
+    """A carried set holding a constant row (an x_0 row, getWLc rows 2..5, or the
+    omega row of x_1, which B does not reach) is rejected, never solved with a
+    garbage normal: same flags and optimum as with no workspace."""
+    N, B = 20, 64
+    cfg, _ = cfgs(N, 2)
+    x = T(O.scenario_x0(np.arange(B)).T)
+    ws = np.full((2 * (N + 1), B), -1, dtype=np.int32)
+    for s in range(B):                        # slot 0: u-bound rows plus one constant row
+        rows = [6 * j + 1 for j in range(1, 8)] + [2 + (s % 4) if s % 5 else 9]
+        ws[:len(rows), s] = rows
+        ws[N, s] = len(rows)
+    rho0, uo0 = ctl.initial_state(x, cfg)
+    ref = ctl.step(x, rho0.clone(), uo0.clone(), cfg)
+    out = ctl.step(x, rho0.clone(), uo0.clone(), cfg, active_ws=T(ws).to(torch.int32))
+    assert torch.equal(out["exitflag"], ref["exitflag"])
+    assert torch.max(torch.abs(out["U"] - ref["U"])).item() <= U_TOL * cfg.umax
+
+
+def test_closed_loop_bitwise_deterministic(ctl):
+    """Two identical closed loops of the bench (B = 40000 scenarios, carried
+    workspace, 10 steps) agree bit for bit: no result depends on LDS a launch
+    did not write (a stale read of rinfo[-1] once made 5-50 scenarios differ)."""
+    N, B, K = 20, 40000, 10
+    cfg, _ = cfgs(N, 2)
+
+    def loop():
+        x = T(O.scenario_x0(np.arange(B)).T)
+        rho, uo = ctl.initial_state(x, cfg)
+        ws = ctl.new_active_ws(B, cfg)
+        Us = []
+        for _ in range(K):
+            out = ctl.step(x, rho, uo, cfg, active_ws=ws)
+            Us.append(out["U"].clone())
+            x = out["x_next"].clone()
+        return torch.stack(Us), rho.clone(), ws.clone()
+
+    a, b = loop(), loop()
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
+
+
 def test_step_workspace_roundtrip_host(ctl):
     """ntm_mpc_step_ws (host buffers) == ntm_mpc_step_ws_device, workspace included."""
     N, B = 20, 32
