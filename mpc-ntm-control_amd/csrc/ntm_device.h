@@ -1820,7 +1820,15 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     int* const colrow = perm + (N + 1);                    // compact column -> row ending there
     bool sq = false;                                       // echelon path (k = nF - nS <= 1)
     int nc = -1;                                           // k = 1: the non-pivot compact column
+    int xb = -1;                                           // one collision: the row left out of the triangle
     const int kdim = nF - nS;
+    // Long horizons with rate rows (config 5) mostly give square sets with ONE
+    // collision: two general rows (a rate row and a state row of the same stage)
+    // end in the same free column, and one column has no row ending there (83% of
+    // the N=50 mode-3 optima, none at N=20 mode 2).  Leaving one of the two rows out
+    // makes the rest echelon with k = 1 (the hole as the non-pivot column); the row
+    // left out then fixes the step along the null vector instead of the cost.
+    constexpr bool kCollision = W::kNN == 0 || W::kNN > 32;
     if ((kdim == 1 || (kdim == 0 && nS > 0)) && !collide) {
         const unsigned long long fm = bal >> (lane & ~(P - 1));   // bit j: variable j is free
         int lastf = -1;
@@ -1846,6 +1854,17 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             nc = kdim ? uni<P>((int)__ffsll((long long)(holes >> (lane & ~(P - 1)))) - 1) : -1;
             if (l < nS) perm[l] = colrow[l + ((nc >= 0 && l >= nc) ? 1 : 0)];
             NTM_WSYNC();
+        } else if (kCollision && kdim == 0 && (int)__popcll(holes) == 1 &&
+                   (__ballot(l < nS && lastf < 0) & gmask) == 0) {
+            // one row does not own its last column (the column's owner is the last writer)
+            const unsigned long long orph = __ballot(l < nS && colrow[lastf < 0 ? 0 : lastf] != l) & gmask;
+            if ((int)__popcll(orph) == 1) {
+                sq = true;
+                nc = uni<P>((int)__ffsll((long long)(holes >> (lane & ~(P - 1)))) - 1);
+                xb = uni<P>((int)__ffsll((long long)(orph >> (lane & ~(P - 1)))) - 1);
+                if (l < nS - 1) perm[l] = colrow[l + (l >= nc ? 1 : 0)];
+                NTM_WSYNC();
+            }
         }
     }
     NTM_ACC(ST_C_SQ, tp);
@@ -1931,7 +1950,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         // Sorted E over the pivot columns (row t = general row perm[t] ends in pivot
         // column pc(t) = t + (t >= nc); lower triangular, n x n row-major at Lp[t LD + u]),
         // the non-pivot column e_c (k = 1) and h
-        const int n = nS;
+        const int n = nS - (xb >= 0 ? 1 : 0);
         auto pc = [&](int u) { return u + ((nc >= 0 && u >= nc) ? 1 : 0); };
         for (int idx = l; idx < n * n; idx += P) {
             const int t = idx / n, u = idx - t * n;
@@ -1942,6 +1961,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             acc = hs_of(perm[l]);
             if (nc >= 0 && nc < pc(l)) acz = -gen_n(perm[l], w.fidx()[nc]);
         }
+        const double hxb = (kCollision && xb >= 0) ? hs_of(xb) : 0.0;   // before w.Phi() is reused
         NTM_WSYNC();
         if (l < n) sq_id = 1.0 / Lp[l * LD + l];
         NTM_ACC(ST_S_E, tp);
@@ -1968,7 +1988,15 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         const double zs = __shfl(zz, (l < N && !fixed) ? rk : 0, P);
         const double v0 = fixed ? vb : ((fpos == nc) ? 0.0 : xs);
         vfin = v0;
-        if (ok && nc >= 0) {
+        if (kCollision && ok && xb >= 0) {
+            // the row left out fixes the step along Z: n_B' (V_0 + w Z) = h_B
+            const double zv = fixed ? 0.0 : ((fpos == nc) ? 1.0 : zs);
+            const double nb = (l < N && !fixed) ? gen_n(xb, l) : 0.0;
+            const double b0 = gsum<P>(nb * v0), b1 = gsum<P>(nb * zv);
+            ok = b1 != 0.0 && isfinite(b1) && isfinite(b0);
+            const double wv = ok ? (hxb - b0) / b1 : 0.0;
+            vfin = v0 + wv * zv;
+        } else if (ok && nc >= 0) {
             // k = 1: the minimum along V_0 + w Z, Z = e_c + Z_p:
             //   w = -(2 yz' Om (y0 + e - r)) / (2 yz' Om yz), y0 = Gamma D V_0, yz = Gamma D Z
             const double zv = fixed ? 0.0 : ((fpos == nc) ? 1.0 : zs);
@@ -2275,14 +2303,32 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             // sorted order), back substitution; lane t owns row t and grad at f_t
             if (l < N && !fixed) w.d()[fpos] = res;
             NTM_WSYNC();
-            double acc = (l < nS) ? w.d()[l + ((nc >= 0 && l >= nc) ? 1 : 0)] : 0.0, mu = 0.0;
-            for (int u = nS - 1; u >= 0; --u) {
+            const int n = nS - (xb >= 0 ? 1 : 0);
+            const int pl = l + ((nc >= 0 && l >= nc) ? 1 : 0);       // lane t's pivot column
+            double acc = (l < n) ? w.d()[pl] : 0.0, mu = 0.0;
+            // one collision: a second right-hand side, the left-out row B at the pivot columns
+            double acb = (kCollision && xb >= 0 && l < n) ? gen_n(xb, w.fidx()[pl]) : 0.0, mb = 0.0;
+            for (int u = n - 1; u >= 0; --u) {
                 const double eu = (l < u) ? Lp[u * LD + l] : 0.0;
                 const double mu_u = gbcast<P>(acc * sq_id, u);
                 if (l == u) mu = mu_u;
                 acc -= eu * mu_u;
+                if (kCollision && xb >= 0) {
+                    const double mb_u = gbcast<P>(acb * sq_id, u);
+                    if (l == u) mb = mb_u;
+                    acb -= eu * mb_u;
+                }
             }
-            if (l < nS) w.np()[perm[l]] = mu;
+            if (kCollision && xb >= 0) {
+                // mu = a - mu_B b; the hole column's equation gives mu_B
+                const double eh = (l < n && nc < pl) ? gen_n(perm[l], w.fidx()[nc]) : 0.0;
+                const double sa = gsum<P>(eh * mu), sb = gsum<P>(eh * mb);
+                const double den = gen_n(xb, w.fidx()[nc]) - sb;
+                const double muB = (w.d()[nc] - sa) / den;
+                mu -= muB * mb;
+                if (l == 0) w.np()[xb] = muB;
+            }
+            if (l < n) w.np()[perm[l]] = mu;
             NTM_WSYNC();
         }
         NTM_ACC(ST_K_MU, tp);
@@ -2331,8 +2377,10 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         int mpos = 0x7fffffff;
         bool has = false;
         if (l < nS) { mval = w.np()[l]; mpos = w.sidx()[l]; has = true; }
+        if (!(fabs(mval) < kInf)) mval = -1e300;         // a non-finite multiplier fails the dual check
         if (fixed) {
             double lam = res / w.hv()[l];
+            if (!(fabs(lam) < kInf)) lam = -1e300;
             if (!has || lam < mval) { mval = lam; mpos = w.fx()[l] - 1; }
             has = true;
         }

@@ -37,7 +37,7 @@ def shift(S, N):
         blk, rr = divmod(r, 6)
         if r >= 6 * N:                      # terminal rows -> stage N-1, and kept
             out.update((6 * (N - 1) + 2 + (r - 6 * N), r))
-        elif blk >= 1:
+        elif blk >= 2 or (blk == 1 and rr < 2):   # x_1's state rows would become x_0 rows: dropped
             out.add(r - 6)
         if blk == N - 1 and rr < 2:        # the old last input's bounds are kept
             out.add(r)
