@@ -2030,7 +2030,6 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         if (!ok) fk = 3;
         NTM_ACC(ST_S_Y, tp);
     } else if (fused) {
-        // E rows over the free variables (one entry per lane) and h; the trailing    } else if (fused) {
         // E rows over the free variables (one entry per lane) and h; the trailing
         // block of A is zero and is never stored (the elimination starts it at 0)
         for (int idx = l; idx < nF * nS; idx += P) {

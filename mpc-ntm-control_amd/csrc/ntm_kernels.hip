@@ -547,6 +547,9 @@ int launch_step(ntm_ctx* ctx, const Prob& pb, int64_t B, const double* x_k, doub
                 int32_t* active_ws, hipStream_t st) {
     constexpr int G = 64 / P;
     size_t lds = (size_t)G * ws_bytes(pb.N);
+#ifdef NTM_LDS_PAD
+    lds += NTM_LDS_PAD;   // occupancy study only (tools/occupancy_study.sh): fewer scenarios per CU
+#endif
     int rc = set_lds(ctx, k_mpc_step<P, NN>, lds);
     if (rc) return rc;
     int64_t blocks = (B + G - 1) / G;
