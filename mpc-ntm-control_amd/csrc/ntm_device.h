@@ -626,13 +626,48 @@ __device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l) {
 // free response e = Phi x_k + Lambda (the x-dependent part of NTM_MPC_Sim.m:121
 // and of c + W x_k at :97)
 template <int P, class W>
-__device__ __forceinline__ void free_response(const W& w, double x0, double x1, int l) {
+__device__ __forceinline__ void free_response(const W& w, double x0, double x1, int l, const Prob* pw = nullptr) {
     for (int i = l; i < w.n(); i += P) {
         const double* Ph = w.Phi() + 4 * i;
-        w.e()[2 * i] = (Ph[0] * x0 + Ph[2] * x1) + w.Lam()[2 * i];
-        w.e()[2 * i + 1] = (Ph[1] * x0 + Ph[3] * x1) + w.Lam()[2 * i + 1];
+        const double e0 = (Ph[0] * x0 + Ph[2] * x1) + w.Lam()[2 * i];
+        const double e1 = (Ph[1] * x0 + Ph[3] * x1) + w.Lam()[2 * i + 1];
+        w.e()[2 * i] = e0;
+        w.e()[2 * i + 1] = e1;
+        if (pw) {
+            // Om (e_i - r) per stage for the scaling pass's F (scratch in w.xp(): the
+            // rollout consumed it and rewrites it; the re-solve recomputes it)
+            const double d0 = e0 - pw->r[0], d1 = e1 - pw->r[1];
+            w.xp()[2 * i] = pw->Q[0] * d0 + pw->Q[1] * d1;
+            w.xp()[2 * i + 1] = pw->Q[2] * d0 + pw->Q[3] * d1;
+        }
     }
     NTM_WSYNC();
+}
+
+// sum_{imin <= i < n} a_i' c_i over 2-vectors stored at stride 2 (c = Om b precomputed)
+template <int CH>
+__device__ __forceinline__ double dot_rows2(const double* a, const double* c, int n, int imin) {
+    double s = 0.0;
+    for (int i0 = 0; i0 < n; i0 += CH) {
+        double a0[CH], a1[CH], c0[CH], c1[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int i = i0 + u;
+            const bool in = i < n;
+            a0[u] = in ? a[2 * i] : 0.0;
+            a1[u] = in ? a[2 * i + 1] : 0.0;
+            c0[u] = in ? c[2 * i] : 0.0;
+            c1[u] = in ? c[2 * i + 1] : 0.0;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int i = i0 + u;
+            const double t = a0[u] * c0[u] + a1[u] * c1[u];
+            s += (i >= imin && i < n) ? t : 0.0;
+        }
+    }
+    return s;
 }
 
 // ---------------------------------------------------------------------------
@@ -717,7 +752,7 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
     if (l < N) {
         // one pass over Gamma's column l: the Gram diagonal G_ll and F_l = 2 Gamma_l' Om (e - r)
         const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
-        const double r0 = pb.r[0], r1 = pb.r[1];
+        const double* om = w.xp();               // Om (e_i - r), from free_response
         double s = 0.0, fs = 0.0;
         constexpr int CH = 4;
         for (int i0 = 0; i0 < N; i0 += CH) {     // fixed trip count, terms i < l masked; batched loads
@@ -728,8 +763,8 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
                 const bool in = i < N;
                 ga[u] = in ? cj[2 * i] : 0.0;
                 gb[u] = in ? cj[2 * i + 1] : 0.0;
-                ea[u] = in ? w.e()[2 * i] : 0.0;
-                eb[u] = in ? w.e()[2 * i + 1] : 0.0;
+                ea[u] = in ? om[2 * i] : 0.0;
+                eb[u] = in ? om[2 * i + 1] : 0.0;
             }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -739,8 +774,7 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
                 const double o0 = q00 * g0 + q01 * g1;
                 const double o1 = q10 * g0 + q11 * g1;
                 const double t = g0 * o0 + g1 * o1;
-                const double e0 = ea[u] - r0, e1 = eb[u] - r1;
-                const double tf = g0 * (q00 * e0 + q01 * e1) + g1 * (q10 * e0 + q11 * e1);
+                const double tf = g0 * ea[u] + g1 * eb[u];
                 const bool on = i >= l && i < N;
                 if (on) bad |= !isfinite(g0) || !isfinite(g1);
                 s += on ? t : 0.0;
@@ -1870,10 +1904,18 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     NTM_ACC(ST_C_SQ, tp);
     // --- g_F (lane a = compact index) ---
     double gl = 0.0;
+    if (!sq) {                                            // Om z in place, once per stage (z is dead after g_F)
+        if (l < N) {
+            const double z0 = w.xp()[2 * l], z1 = w.xp()[2 * l + 1];
+            w.xp()[2 * l] = q00 * z0 + q01 * z1;
+            w.xp()[2 * l + 1] = q10 * z0 + q11 * z1;
+        }
+        NTM_WSYNC();
+    }
     if (!sq && l < nF) {
         const int ja = w.fidx()[l];
         const double* ca = w.Gt() + w.gidx(2 * ja, ja) - 2 * ja;   // ca[r] = gt(r, ja), r >= 2 ja
-        const double g2 = qdot_rows<4>(ca, w.xp(), N, ja, q00, q01, q10, q11);   // terms i < ja masked
+        const double g2 = dot_rows2<4>(ca, w.xp(), N, ja);          // terms i < ja masked
         gl = w.D()[ja] * (2 * g2);
     }
     // Bordered KKT system (fused path): rows 0..nF-1 free variables, nF..nt-1 general
@@ -2290,10 +2332,17 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         ok = vf.p == 0;
         NTM_ACC(ST_K_CHK, tp);
         // gradient G~V + F~ = D (2 Gamma' Om y) + F~
+        // (y is dead after the primal check: Om y in place, once per stage)
+        if (l < N) {
+            const double y0 = w.xp()[2 * l], y1 = w.xp()[2 * l + 1];
+            w.xp()[2 * l] = q00 * y0 + q01 * y1;
+            w.xp()[2 * l + 1] = q10 * y0 + q11 * y1;
+        }
+        NTM_WSYNC();
         double res = 0.0;
         if (l < N) {
             const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;
-            const double g2 = qdot_rows<4>(cl, w.xp(), N, l, q00, q01, q10, q11);   // terms i < l masked
+            const double g2 = dot_rows2<4>(cl, w.xp(), N, l);   // terms i < l masked
             res = w.D()[l] * (2 * g2) + w.F()[l];
         }
         NTM_ACC(ST_K_GRAD, tp);
@@ -2537,7 +2586,7 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
     NTM_T0(tq);
     lift_phase<P>(pb, w, l);
     NTM_ACC(ST_LIFT, tq);
-    free_response<P>(w, x0, x1, l);          // F is formed with the Jacobi scaling below
+    free_response<P>(w, x0, x1, l, &pb);     // F is formed with the Jacobi scaling below
     NTM_ACC(ST_COST, tq);
     const bool full = pb.mode >= NTM_MODE_FULL;        // state rows present
     int flag, q = 0, ns = 0;
