@@ -1904,18 +1904,10 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     NTM_ACC(ST_C_SQ, tp);
     // --- g_F (lane a = compact index) ---
     double gl = 0.0;
-    if (!sq) {                                            // Om z in place, once per stage (z is dead after g_F)
-        if (l < N) {
-            const double z0 = w.xp()[2 * l], z1 = w.xp()[2 * l + 1];
-            w.xp()[2 * l] = q00 * z0 + q01 * z1;
-            w.xp()[2 * l + 1] = q10 * z0 + q11 * z1;
-        }
-        NTM_WSYNC();
-    }
     if (!sq && l < nF) {
         const int ja = w.fidx()[l];
         const double* ca = w.Gt() + w.gidx(2 * ja, ja) - 2 * ja;   // ca[r] = gt(r, ja), r >= 2 ja
-        const double g2 = dot_rows2<4>(ca, w.xp(), N, ja);          // terms i < ja masked
+        const double g2 = qdot_rows<4>(ca, w.xp(), N, ja, q00, q01, q10, q11);   // terms i < ja masked
         gl = w.D()[ja] * (2 * g2);
     }
     // Bordered KKT system (fused path): rows 0..nF-1 free variables, nF..nt-1 general

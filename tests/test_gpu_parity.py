@@ -190,6 +190,19 @@ def test_quadprog_matches_oracle(ctl, mode):
                                          (50, 2, True), (20, 3, False), (20, 3, True), (4, 3, False),
                                          (50, 3, True), (1, 2, False), (1, 1, True), (64, 2, True)])
 def test_step_teacher_forced(ctl, N, mode, warm):
+    _teacher_forced(ctl, N, mode, warm)
+
+
+# Non-identity stage weights: the reference's Omega = blkdiag(Q, ..., Q) (NTM_MPC_Sim.m:59,
+# 67-70) with a coupled symmetric positive-definite Q (row-major 2x2), so the per-stage
+# Om products of the device (free response, certificate gradient, Gram terms) are
+# exercised off the diagonal; another reference state r as well
+@pytest.mark.parametrize("N,mode,warm", [(20, 2, True), (20, 1, False), (50, 2, False), (3, 2, False)])
+def test_step_teacher_forced_weighted(ctl, N, mode, warm):
+    _teacher_forced(ctl, N, mode, warm, k_sim=6, Q=(2.0e4, 3.0, 3.0, 2.0e-2), r=(0.09, 900 * 2 * math.pi))
+
+
+def _teacher_forced(ctl, N, mode, warm, k_sim=None, **kw):
     """Each step, the GPU and the oracle get identical (x_k, rho, U_old); with
     warm=True the GPU also carries its active-set workspace from step to step
     (ntm_mpc_step_ws_device), which must not change the answer.
@@ -203,8 +216,9 @@ def test_step_teacher_forced(ctl, N, mode, warm):
     the same path are compared directly (>= 90% of them must have), and the
     others against the oracle re-run along the GPU's path (the GPU's
     inner-iteration count, no early stop), to the same tolerance."""
-    B, k_sim = (48, 12) if N < 50 else ((48, 4) if N == 50 else (16, 3))
-    cfg, ocfg = cfgs(N, mode)
+    B, ks = (48, 12) if N < 50 else ((48, 4) if N == 50 else (16, 3))
+    k_sim = min(ks, k_sim) if k_sim else ks
+    cfg, ocfg = cfgs(N, mode, **kw)
     x = O.scenario_x0(np.arange(B)).T if mode else np.tile(O.REFERENCE_X0[:, None], (1, B))
     rho, Uo = cbind.initial_state(x, ocfg)
     ws = ctl.new_active_ws(B, cfg) if warm else None
