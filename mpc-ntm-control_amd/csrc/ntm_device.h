@@ -538,6 +538,34 @@ __device__ __forceinline__ double gamma_row_dot(const W& w, int r, const double*
     return y;
 }
 
+// Gamma_r v1 and Gamma_r v2 in one pass over row r (its loads shared)
+template <int CH, class W>
+__device__ __forceinline__ void gamma_row_dot2(const W& w, int r, const double* v1, const double* v2, double& y1,
+                                               double& y2) {
+    const int n = w.n(), jm = r >> 1;
+    const double* gr = w.Gt() + r;
+    y1 = 0.0;
+    y2 = 0.0;
+    for (int j0 = 0; j0 < n; j0 += CH) {
+        double g[CH], x1[CH], x2[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int j = j0 + u;
+            const bool in = j < n;
+            g[u] = in ? gr[w.gidx(0, j)] : 0.0;
+            x1[u] = in ? v1[j] : 0.0;
+            x2[u] = in ? v2[j] : 0.0;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const double gm = (j0 + u <= jm) ? g[u] : 0.0;
+            y1 += gm * x1[u];
+            y2 += gm * x2[u];
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // L2: lifted prediction  (Rho_to_PhiGammaLambda.m:17-52, CANON D4/D6)
 // ---------------------------------------------------------------------------
@@ -2040,8 +2068,10 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             }
             NTM_WSYNC();
             for (int r = l; r < 2 * N; r += P) {
-                w.xp()[r] = gamma_row_dot<4>(w, r, w.U());
-                w.Phi()[r] = gamma_row_dot<4>(w, r, w.d());      // scratch (hs_of is done with it)
+                double ya, yb;
+                gamma_row_dot2<4>(w, r, w.U(), w.d(), ya, yb);
+                w.xp()[r] = ya;
+                w.Phi()[r] = yb;                                 // scratch (hs_of is done with it)
             }
             NTM_WSYNC();
             double num = 0.0, den = 0.0;
