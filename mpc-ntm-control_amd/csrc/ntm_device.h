@@ -123,13 +123,7 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        ST_SC_COL, ST_SC_ROW, ST_SC_END, ST_L_COEF, ST_L_LOOP };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 constexpr int kMaxNT = 32;         // explicit R^{-1} in GI up to this horizon (WS::useT)
-constexpr int kRepairs = 8;
-// long horizons (N > 32): a GI solve costs ~14 certified re-solves there (N = 50), so
-// failed candidates get more single-row repairs before the fallback
-#ifndef NTM_REPAIRS_LONG
-#define NTM_REPAIRS_LONG 8
-#endif
-constexpr int kRepairsLong = NTM_REPAIRS_LONG;
+constexpr int kRepairs = 8;   // also at N = 50: 16 / 32 were no faster in mode 2, 6% / 10% slower in mode 3
 // A constant row (Lin_i = 0: the x_0 rows of getWLc, state rows Gamma doesn't
 // reach) is violated when b_i < -kConstTol (D22, oracle CONST_ROW_TOL): the same
 // absolute 1e-9 the KKT certificate allows on a unit-scale row.  An exact test
@@ -2676,7 +2670,7 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                         if (rep > 0) NTM_CNT(CN_REPAIR);
                         break;
                     }
-                    bool stop = rep >= (N > 32 ? kRepairsLong : kRepairs) || rep < 0 || fk == 3;   // rep < 0: the shifted set failed
+                    bool stop = rep >= kRepairs || rep < 0 || fk == 3;   // rep < 0: the shifted set failed
                     if (!stop && (fk == 2 || fk == 4)) {   // primal: add the most violated row
                         if (l < cq) w.aflag()[w.act()[l]] = kActiveRow;
                         NTM_WSYNC();
