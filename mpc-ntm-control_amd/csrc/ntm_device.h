@@ -777,63 +777,6 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
     const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
     int bad = 0;
     NTM_T0(tsc);
-#if NTM_SPLIT_COL
-    if (P == 64 && N <= 32) {
-        // the same column pass split over the two wave halves: lane c < 32 sums
-        // stages [0, H), lane c + 32 stages [H, N) of column c; one permlane32
-        // swap joins the halves (half the dependent LDS-load chain per lane)
-        constexpr int CH = 4;
-        const int NC = (N + CH - 1) / CH, HC = (NC + 1) / 2;
-        const int c = l & 31, hi = l >> 5;
-        const int ib = hi ? HC * CH : 0;
-        const int cc = c < N ? c : N - 1;         // idle columns read a real column (masked)
-        const double* cj = w.Gt() + w.gidx(2 * cc, cc) - 2 * cc;
-        const double* om = w.xp();
-        double s = 0.0, fs = 0.0;
-        for (int k = 0; k < HC; ++k) {
-            const int i0 = ib + k * CH;
-            double ga[CH], gb[CH], ea[CH], eb[CH];
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-                const int i = i0 + u;
-                const bool in = i < N && c < N;
-                ga[u] = in ? cj[2 * i] : 0.0;
-                gb[u] = in ? cj[2 * i + 1] : 0.0;
-                ea[u] = in ? om[2 * i] : 0.0;
-                eb[u] = in ? om[2 * i + 1] : 0.0;
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < CH; ++u) {
-                const int i = i0 + u;
-                const double g0 = ga[u], g1 = gb[u];
-                const double o0 = q00 * g0 + q01 * g1;
-                const double o1 = q10 * g0 + q11 * g1;
-                const double t = g0 * o0 + g1 * o1;
-                const double tf = g0 * ea[u] + g1 * eb[u];
-                const bool on = i >= c && i < N && c < N;
-                if (on) bad |= !isfinite(g0) || !isfinite(g1);
-                s += on ? t : 0.0;
-                fs += on ? tf : 0.0;
-            }
-        }
-        double s0, s1, f0, f1;
-        pair_d<32>(s, s0, s1);
-        pair_d<32>(fs, f0, f1);
-        s = s0 + s1;
-        fs = f0 + f1;
-        if (l < N) {
-            double g = 2 * s;
-            double Dl = (g > 0.0 && g < kInf) ? rsqrt_nr(g) : 1.0;
-            w.D()[l] = Dl;
-            double f = (2 * fs) * Dl;
-            bad |= !isfinite(f) || !isfinite(Dl);
-            w.F()[l] = f;
-            w.vlo()[l] = -((-pb.umin) / Dl);
-            w.vhi()[l] = pb.umax / Dl;
-        }
-    } else
-#endif
     if (l < N) {
         // one pass over Gamma's column l: the Gram diagonal G_ll and F_l = 2 Gamma_l' Om (e - r)
         const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
