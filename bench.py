@@ -14,8 +14,12 @@ gathered over RCCL at the end of the timed region (the end-of-batch gather).
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line (bench contract).  roofline.achieved uses this
-build's own algorithmic flop count (ntm_mpc/flops.py)
-over the kernel's HIP-event-timed average duration.
+build's own algorithmic flop count (ntm_mpc/flops.py),
+driven by the kernel's own solver counters accumulated over exactly the K
+timed launches, over the kernel's HIP-event-timed average duration.  A second
+leg ("disturbed") runs the same workload with the scenario generator on
+(per-step w disturbance sigma_w = 1e-3 m and +-10% j_BS / w_dep plasma
+scenarios) and reports its rate and warm-start statistics.
 """
 from __future__ import annotations
 
@@ -44,6 +48,10 @@ def parse():
     ap.add_argument("--N", type=int, default=20)
     ap.add_argument("--mode", type=int, default=2)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-disturbed", action="store_true", help="skip the disturbed-loop leg")
+    ap.add_argument("--sigma-w", type=float, default=1e-3, help="disturbed leg: w disturbance per step [m]")
+    ap.add_argument("--spread", type=float, default=0.1, help="disturbed leg: j_BS / w_dep spread over scenarios")
+    ap.add_argument("--verify", type=int, default=64, help="scenarios rank 0 recomputes after the gather")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample length")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse the multi-rank "
@@ -61,52 +69,180 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(N, mode, target_s):
+def _cpu_threads():
+    """Threads of the CPU leg: the box's CPU share (OMP_NUM_THREADS, which the GPU
+    pool sets to 16 per GPU and asks jobs to keep), bounded by this process's
+    CPU affinity.  nproc is recorded alongside."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    want = int(os.environ.get("OMP_NUM_THREADS", "0")) or aff
+    return max(1, min(want, aff)), aff
+
+
+def cpu_baseline(N, mode, target_s, warm_steps=5, timed_steps=20):
     """C restatement of the oracle (oracle/ntm_oracle.c, the "port"), OpenMP over
-    scenarios on this host, timed on a bounded sample of the same workload; plus
-    the same on one core and the NumPy oracle (single thread, the interpreted
-    stand-in for MATLAB) on a few scenarios (BASELINE.md CPU-baseline plan)."""
+    scenarios on this host, timed on a bounded sample of the same workload and
+    the same closed-loop steps as the GPU (steps warm_steps+1 .. warm_steps+
+    timed_steps, after warm_steps untimed ones); plus the same on one core and
+    the NumPy oracle (single thread, the interpreted stand-in for MATLAB).  The
+    port solves every QP cold: Goldfarb-Idnani from the empty set plus the exact
+    active-set polish, no carried active sets (the GPU kernel's certified
+    warm-start re-solves are its own algorithm)."""
     import numpy as np
     from oracle import cbind
     from oracle import ntm_oracle as O
     import ntm_mpc
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    threads, aff = _cpu_threads()
     cfg = O.Config(N=N, mode=mode)
-    k = 2
 
-    def timed(B, nthreads):
-        x0 = ntm_mpc.scenarios_x0(0, B)
+    def steady(B, nthreads, steps):
+        x = ntm_mpc.scenarios_x0(0, B)
+        x = np.ascontiguousarray(x)
+        rho, uo = cbind.initial_state_gen(x, cfg)
+        for _ in range(warm_steps):                       # untimed: steps 1..warm_steps
+            r = cbind.step(x, rho, uo, cfg, nthreads=nthreads)
+            x, rho, uo = r["x_next"], r["rho"], r["U_old"]
         t = time.perf_counter()
-        cbind.run(x0, cfg, k, nthreads=nthreads)
+        for _ in range(steps):
+            r = cbind.step(x, rho, uo, cfg, nthreads=nthreads)
+            x, rho, uo = r["x_next"], r["rho"], r["U_old"]
         return time.perf_counter() - t
 
+    steady(threads, threads, 1)                               # load the library, start the thread pool
     B = 64 * threads
-    dt = timed(B, threads)
-    B2 = int(min(400_000, max(B, B * target_s / max(dt, 1e-3))))
-    dt = timed(B2, threads)
-    b1 = 64
-    d1 = timed(b1, 1)
-    b1 = int(min(20_000, max(b1, b1 * 3.0 / max(d1, 1e-3))))   # ~3 s on one core
-    d1 = timed(b1, 1)
+    dt = steady(B, threads, 2)
+    B2 = int(min(400_000, max(B, B * 2 * target_s / (timed_steps * max(dt, 1e-3)))))
+    dt = steady(B2, threads, timed_steps)
+    b1 = 8
+    d1 = steady(b1, 1, 2)
+    b1 = int(min(20_000, max(b1, b1 * 2 * 3.0 / (timed_steps * max(d1, 1e-3)))))   # ~3 s on one core
+    d1 = steady(b1, 1, timed_steps)
     ph, nb = O.Physics(), 30
     t = time.perf_counter()
     for s in range(nb):                                         # NumPy oracle, one step each
         x = ntm_mpc.scenarios_x0(s, 1)[:, 0]
         O.mpc_step(x, O.initial_rho(x, ph, cfg), np.full(N, np.inf), ph, cfg)
     dpy = time.perf_counter() - t
-    return {"value": B2 * k / dt, "unit": "MPC steps/s", "cores": threads, "kind": "port",
-            "sample": f"{B2} scenarios x {k} closed-loop steps (ids 0..{B2 - 1}), N={N}, mode={mode}, "
+    return {"value": B2 * timed_steps / dt, "unit": "MPC steps/s", "cores": threads, "kind": "port",
+            "sample": f"{B2} scenarios (ids 0..{B2 - 1}) x closed-loop steps {warm_steps + 1}-"
+                      f"{warm_steps + timed_steps} (after {warm_steps} untimed), N={N}, mode={mode}, "
                       f"{threads} OpenMP threads, {dt:.1f} s",
-            "one_core_value": b1 * k / d1, "one_core_sample": f"{b1} scenarios x {k} steps, 1 thread, {d1:.1f} s",
+            "solver": "C port of the oracle: cold Goldfarb-Idnani per QP + exact active-set polish, "
+                      "no carried active sets",
+            "one_core_value": b1 * timed_steps / d1,
+            "one_core_sample": f"{b1} scenarios x steps {warm_steps + 1}-{warm_steps + timed_steps}, 1 thread, "
+                               f"{d1:.1f} s",
             "interpreted_numpy_value": nb / dpy,
-            "interpreted_sample": f"NumPy oracle, {nb} scenarios x 1 step, 1 thread, {dpy:.1f} s",
-            "host": {"nproc": os.cpu_count(), "cpu_model": _cpu_model()}}
+            "interpreted_sample": f"NumPy oracle, {nb} scenarios x 1 step (cold), 1 thread, {dpy:.1f} s",
+            "host": {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": _cpu_model(),
+                     "note": "threads = the GPU pool's per-GPU CPU share (OMP_NUM_THREADS), not every core "
+                             "of the shared host: the pool asks jobs to keep to it"}}
+
+
+def _workload(N, mode, B):
+    kind = {0: "unconstrained LQ", 1: "box-constrained u", 2: "full getWLc constraints",
+            3: "full getWLc + input-rate rows"}[mode]
+    cfgs = {(20, 2, 100_000): "BASELINE config 3", (20, 1, 1024): "BASELINE config 2",
+            (50, 3, 100_000): "BASELINE config 5 (rate rows)", (50, 2, 100_000): "BASELINE config 5 shape (N=50)",
+            (10, 0, 1): "BASELINE config 1"}
+    tag = cfgs.get((N, mode, B), "custom")
+    return f"{tag}: LPV-MPC closed-loop step, N={N}, {kind}, B={B} per GPU, fp64"
+
+
+def _run_leg(ctl, cfg, B, K, W, x0, rank, world, gen=None, collect=False):
+    """W untimed warmup steps then K timed steps of the closed loop through the
+    step entry point, the solver counters accumulated over exactly the K timed
+    launches.  Returns timing, per-step counters and (collect) the histories."""
+    import torch
+    import torch.distributed as dist
+    from ntm_mpc.api import STATS_ROWS
+    dev = f"cuda:{ctl.device}"
+    ctl.set_scenarios(gen)
+    x = x0
+    rho, U_old = ctl.initial_state(x, cfg)
+    active_ws = ctl.new_active_ws(B, cfg)       # last two active sets, carried step to step (DESIGN.md §4)
+    outs = [None, None]
+
+    def one_step(i, xin):
+        if gen is not None:
+            gen.k0 = i                          # the plant step's time index
+            ctl.set_scenarios(gen)
+        out = ctl.step(xin, rho, U_old, cfg, out=outs[i & 1], active_ws=active_ws)
+        outs[i & 1] = out
+        return out
+
+    for i in range(W):
+        x = one_step(i, x)["x_next"].clone()
+    N = cfg.N
+    hist = None
+    if collect:
+        hist = {"uk": torch.empty(K, B, dtype=torch.float64, device=dev),
+                "Uk": torch.empty(K, N, B, dtype=torch.float64, device=dev),
+                "xk": torch.empty(K + 1, 2, B, dtype=torch.float64, device=dev),
+                "wpred": torch.empty(K, N + 1, B, dtype=torch.float64, device=dev),
+                "exitflag": torch.empty(K, B, dtype=torch.int32, device=dev),
+                "inner_iters": torch.empty(K, B, dtype=torch.int32, device=dev)}
+        hist["xk"][0].copy_(x)
+    stats = torch.zeros(STATS_ROWS, B, dtype=torch.int32, device=dev)
+    ctl.set_stats(stats)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    xin = x
+    for i in range(K):
+        ev[i][0].record()
+        out = one_step(W + i, xin)
+        ev[i][1].record()
+        if collect:
+            hist["uk"][i].copy_(out["U"][0])
+            hist["Uk"][i].copy_(out["U"])
+            hist["xk"][i + 1].copy_(out["x_next"])
+            hist["wpred"][i].copy_(out["x_pred"][0::2])
+            hist["exitflag"][i].copy_(out["exitflag"])
+            hist["inner_iters"][i].copy_(out["inner_iters"])
+        xin = out["x_next"]
+    return {"t0": t0, "ev": ev, "stats": stats, "out": out, "hist": hist}
+
+
+def _finish_leg(ctl, leg, K):
+    import torch
+    torch.cuda.synchronize()
+    ctl.set_stats(None)
+    ctl.set_scenarios(None)
+    kern_ms = sum(a.elapsed_time(b) for a, b in leg["ev"]) / K
+    B = leg["stats"].shape[1]
+    st = leg["stats"].double().sum(dim=1).cpu().numpy() / (B * K)          # per MPC step
+    flags = leg["out"]["exitflag"]
+    return {"kern_ms": kern_ms, "qps": st[0], "Kgi": st[1], "tries": st[4], "giruns": st[5],
+            "qact": st[2] / st[0], "sgen": st[3] / st[0],
+            "optimal_frac": float((flags == 1).double().mean().item()),
+            "inner_iters_mean": float(leg["out"]["inner_iters"].double().mean().item())}
+
+
+def _verify_gathered(ctl, cfg, B_total, K, W, g, n_verify, seed=12345):
+    """Rank 0: recompute a seeded sample of the gathered scenarios from their
+    global ids alone (one process, one GPU) and require bit-identical histories."""
+    import numpy as np
+    import torch
+    import ntm_mpc
+    rng = np.random.default_rng(seed)
+    ids = np.sort(rng.choice(B_total, size=min(n_verify, B_total), replace=False))
+    x0 = np.concatenate([ntm_mpc.scenarios_x0(int(i), 1) for i in ids], axis=1)
+    x = ctl.tensor(x0)
+    n = len(ids)
+    leg = _run_leg(ctl, cfg, n, K, W, x, 0, 1, collect=True)
+    _finish_leg(ctl, leg, K)
+    sel = torch.as_tensor(ids, device=leg["hist"]["uk"].device)
+    bad = [k for k, v in leg["hist"].items() if not bool((v == g[k].index_select(-1, sel)).all().item())]
+    return {"scenarios": n, "ids_seed": seed, "bitwise_equal": not bad, "mismatched": bad}
 
 
 def main():
     args = parse()
-    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -124,82 +260,44 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
     import ntm_mpc
-    from ntm_mpc import Config, NtmMpc
+    from ntm_mpc import Config, NtmMpc, ScenarioGen
     from ntm_mpc import flops as FL
-    from ntm_mpc.api import STATS_ROWS
+    from ntm_mpc.dist import gather_scenarios
 
     B, N, K, W = args.batch, args.N, args.steps, args.warmup
     cfg = Config(N=N, mode=args.mode)
     ctl = NtmMpc(config=cfg, device=local)
-    dev = f"cuda:{local}"
     # shard: global scenario ids [rank*B, (rank+1)*B)  (shard-invariant inputs)
-    x = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(rank * B, B), local)
-    rho, U_old = ctl.initial_state(x, cfg)
-    active_ws = ctl.new_active_ws(B, cfg)       # last two active sets, carried step to step
-    outs = [None, None]
+    x0 = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(rank * B, B), local)
 
-    def one_step(i, xin):
-        out = ctl.step(xin, rho, U_old, cfg, out=outs[i & 1], active_ws=active_ws)
-        outs[i & 1] = out
-        return out
-
-    # warmup (untimed): also advances the closed loop
-    for i in range(W):
-        x = one_step(i, x)["x_next"].clone()
-    # instrumentation pass (untimed, separate launch on a copy of the state)
-    stats = torch.zeros(STATS_ROWS, B, dtype=torch.int32, device=dev)
-    rho_s, uo_s, ws_s = rho.clone(), U_old.clone(), active_ws.clone()
-    ctl.set_stats(stats)
-    ctl.step(x, rho_s, uo_s, cfg, active_ws=ws_s)
-    ctl.set_stats(None)
-    torch.cuda.synchronize()
-    st = stats.double().sum(dim=1).cpu().numpy()
-    qps, Kgi, tries, giruns = st[0] / B, st[1] / B, st[4] / B, st[5] / B     # per MPC step
-    qact, sgen = st[2] / st[0], st[3] / st[0]                                 # per QP
-    del rho_s, uo_s, ws_s
-
-    hist_u = torch.empty(K, B, dtype=torch.float64, device=dev)
-    hist_x = torch.empty(K, 2, B, dtype=torch.float64, device=dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    leg = _run_leg(ctl, cfg, B, K, W, x0, rank, world, collect=True)
+    # end-of-batch gather of every per-scenario output history (RCCL over xGMI;
+    # gloo rehearsal through host memory), scenario order = global id order
+    g = None
     if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    xin = x
-    for i in range(K):
-        ev[i][0].record()
-        out = one_step(W + i, xin)
-        ev[i][1].record()
-        hist_u[i].copy_(out["U"][0])
-        hist_x[i].copy_(out["x_next"])
-        xin = out["x_next"]
-    # end-of-batch gather of the control sequence and trajectory (RCCL over xGMI)
-    if world > 1 and not rehearsal:
-        g_u = torch.empty(world * K * B, dtype=torch.float64, device=dev)
-        g_x = torch.empty(world * K * 2 * B, dtype=torch.float64, device=dev)
-        dist.all_gather_into_tensor(g_u, hist_u.reshape(-1))
-        dist.all_gather_into_tensor(g_x, hist_x.reshape(-1))
-    elif world > 1:                     # gloo rehearsal: same exchange through host memory
-        g_u = [torch.empty(K * B, dtype=torch.float64) for _ in range(world)]
-        g_x = [torch.empty(K * 2 * B, dtype=torch.float64) for _ in range(world)]
-        dist.all_gather(g_u, hist_u.reshape(-1).cpu())
-        dist.all_gather(g_x, hist_x.reshape(-1).cpu())
+        tot = world * B
+        g = {k: gather_scenarios(v.cpu() if rehearsal else v, tot) for k, v in leg["hist"].items()}
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = time.perf_counter() - leg["t0"]
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else f"cuda:{local}")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / K
-    flags = out["exitflag"]
-    n_opt = int((flags == 1).sum().item())
-    iters = out["inner_iters"].double().mean().item()
+    r = _finish_leg(ctl, leg, K)
+    if g is None:
+        g = leg["hist"]
+    verify = None
+    if rank == 0 and args.verify > 0:
+        gd = {k: v.to(f"cuda:{local}") for k, v in g.items()}
+        verify = _verify_gathered(ctl, cfg, world * B, K, W, gd, args.verify)
+        del gd
+    del g, leg
 
     value = world * B * K / elapsed
-    flop_step = FL.per_step(N, args.mode, qps, tries, giruns, Kgi, qact, sgen)
-    achieved = flop_step * B / (kern_ms * 1e-3) / 1e12
+    flop_step = FL.per_step(N, args.mode, r["qps"], r["tries"], r["giruns"], r["Kgi"], r["qact"], r["sgen"])
+    achieved = flop_step * B / (r["kern_ms"] * 1e-3) / 1e12
     traffic = None
     # PMC-measured HBM bytes per launch of this workload (tools/traffic_run.py,
     # separate FETCH_SIZE / WRITE_SIZE passes): the latest round's file that matches
@@ -225,21 +323,45 @@ def main():
         "dtype": "f64",
         "data": "synthetic: counter-based x0 (w0~U[0.07,0.14] m, omega0~U[0.8,1.2]*2000pi), nominal physics "
                 "NTM_MPC_Sim.m:5-60, closed loop advanced step to step",
-        "config": {"workload": "BASELINE config 3: LPV-MPC closed-loop step, full getWLc constraints, fp64",
+        "config": {"workload": _workload(N, args.mode, B),
                    "scenarios_per_gpu": B, "global_batch": world * B, "N": N, "mode": args.mode, "i_sim": 10,
-                   "parallelism": f"scenario-sharded x{world} (weak), end-of-batch all_gather"
+                   "timed_closed_loop_steps": f"{W + 1}-{W + K}",
+                   "parallelism": f"scenario-sharded x{world} (weak), end-of-batch gather of uk, Uk, xk, wpred, "
+                                  "exitflag, inner_iters"
                        + (" [gloo rehearsal: ranks share devices]" if rehearsal and world > 1 else "")},
         "roofline": {"bound": "valu-fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": ctl.step_kernel_name(B, cfg), "kernel_avg_ms": kern_ms,
+                     "kernel": ctl.step_kernel_name(B, cfg), "kernel_avg_ms": r["kern_ms"],
                      "flop_per_step": flop_step,
+                     "flop_counters": "solver counters of the K timed launches (ntm_ctx_set_stats on in the "
+                                      "timed region)",
                      "hbm_algorithmic_bytes_per_launch": FL.hbm_bytes_per_step(N, workspace=True) * B,
                      "note": "fp64 VALU work (DPP/LDS, no MFMA: DESIGN.md §6); peak = MI355X fp64 vector rate "
                              "(78.6 TF, equal to the fp64 matrix rate)"},
-        "solver": {"inner_iters_mean": iters, "qp_per_step": qps, "warm_verify_per_step": tries,
-                   "gi_solves_per_step": giruns, "gi_iters_per_step": Kgi,
-                   "active_rows_per_qp": qact, "state_rows_per_qp": sgen, "optimal_frac": n_opt / B},
+        "solver": {"inner_iters_mean": r["inner_iters_mean"], "qp_per_step": r["qps"],
+                   "warm_verify_per_step": r["tries"], "gi_solves_per_step": r["giruns"],
+                   "gi_iters_per_step": r["Kgi"], "active_rows_per_qp": r["qact"], "state_rows_per_qp": r["sgen"],
+                   "warm_hit_rate": 1.0 - r["giruns"] / r["qps"], "optimal_frac": r["optimal_frac"]},
+        "gather_verify": verify,
     }
+    if not args.no_disturbed:
+        gen = ScenarioGen(seed=20241220, first_id=rank * B, k0=0, sigma_w=args.sigma_w, sigma_omega=0.0,
+                          jbs_spread=args.spread, wdep_spread=args.spread)
+        dl = _run_leg(ctl, cfg, B, K, W, x0, rank, world, gen=gen)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        d_el = time.perf_counter() - dl["t0"]
+        d = _finish_leg(ctl, dl, K)
+        res["disturbed"] = {
+            "value": world * B * K / d_el, "ms_per_step": d_el / K * 1e3, "kernel_avg_ms": d["kern_ms"],
+            "generator": {"sigma_w_m": args.sigma_w, "jbs_spread": args.spread, "wdep_spread": args.spread,
+                          "seed": 20241220, "disturbance": "Irwin-Hall(4) unit variance x sigma_w per plant step"},
+            "inner_iters_mean": d["inner_iters_mean"], "qp_per_step": d["qps"], "warm_verify_per_step": d["tries"],
+            "gi_solves_per_step": d["giruns"], "gi_iters_per_step": d["Kgi"],
+            "warm_hit_rate": 1.0 - d["giruns"] / d["qps"], "optimal_frac": d["optimal_frac"],
+            "flop_per_step": FL.per_step(N, args.mode, d["qps"], d["tries"], d["giruns"], d["Kgi"], d["qact"],
+                                         d["sgen"])}
     if rank == 0 and not args.no_cpu:
         try:
             res["cpu_baseline"] = cpu_baseline(N, args.mode, args.cpu_seconds)

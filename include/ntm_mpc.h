@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define NTM_MPC_ABI_VERSION 3
+#define NTM_MPC_ABI_VERSION 4   /* v4: ntm_scenario_gen (ABI v3 arrays unchanged) */
 #define NTM_MAX_N 64
 
 /* Physics constants, NTM_MPC_Sim.m:5-22 (same names and units). */
@@ -196,6 +196,42 @@ int ntm_qp_device(ntm_ctx* ctx, int64_t B, int32_t N, int32_t m,
 /* Synthetic scenarios, counter-based and shard-invariant:
  * x0 for global scenario ids first_id .. first_id+B-1 (host array, 2 per scenario). */
 void ntm_scenarios_x0(uint64_t seed, int64_t first_id, int64_t B, double* x0);
+
+/* ---- scenario generator: plasma scenarios and disturbance realisations --- */
+/* North_star's "independent plasma scenarios / disturbance realisations"
+ * (SURVEY.md §8d): per-scenario plasma parameters j_BS and w_dep (NTM_MPC_Sim.m:5-6,
+ * which enter C at :37, B.m:2 and rho3.m:2) and an additive disturbance on the
+ * plant step (NTM_MPC_Sim.m:130).  The controller's model is the scenario's own
+ * plasma (plant = model, D13); the disturbance is the plant's alone.
+ * Counter-based: every value is a function of (seed, global scenario id, time
+ * index) only, so any sharding or batching reproduces the same realisations.
+ *   u(seed, id, k, ch) = splitmix64^3 chain >> 11, times 2^-53 (uniform [0,1));
+ *   n(seed, id, k, c)  = (sum of u at ch = 4c..4c+3 - 2) * sqrt(3): unit variance,
+ *                        zero mean, bounded at +-2 sqrt(3) (Irwin-Hall; + and *
+ *                        only, so host, device and oracles agree bit for bit);
+ *   scenario id: j_BS * (1 + jbs_spread (2 u(id, 0xFFFFFFFF, 0) - 1)),
+ *                w_dep * (1 + wdep_spread (2 u(id, 0xFFFFFFFF, 1) - 1));
+ *   plant step k: x_{k+1} += [sigma_w n(id, k, 0); sigma_omega n(id, k, 1)]. */
+typedef struct {
+    uint64_t seed;
+    int64_t first_id;    /* global id of the batch's scenario 0 (a shard's offset)   */
+    int32_t k0;          /* time index of the next launch's first plant step: the one
+                            plant step of ntm_mpc_step*, k0 .. k0+k_sim-1 in ntm_mpc_run* */
+    int32_t reserved;    /* must be 0                                                */
+    double sigma_w;      /* additive w disturbance per plant step [m], >= 0          */
+    double sigma_omega;  /* additive omega disturbance per plant step [rad/s], >= 0  */
+    double jbs_spread;   /* relative j_BS spread over scenarios, in [0, 1)           */
+    double wdep_spread;  /* relative w_dep spread over scenarios, in [0, 1)          */
+} ntm_scenario_gen;
+/* Attach a generator to the context (copied): subsequent ntm_mpc_init*,
+ * ntm_mpc_step* and ntm_mpc_run* launches use it.  NULL restores the nominal,
+ * disturbance-free plant (the reference's own deterministic loop).  The
+ * function-level entry points (rho, A/B, lift, cost, getWLc, QP) stay nominal. */
+int ntm_ctx_set_scenarios(ntm_ctx* ctx, const ntm_scenario_gen* gen);
+/* Host-side samples of the same generator (no GPU): per scenario
+ * first_id .. first_id+B-1, out4[4s..4s+3] = (j_BS factor, w_dep factor,
+ * n(id, k, 0), n(id, k, 1)). */
+void ntm_scenario_sample(const ntm_scenario_gen* gen, int64_t B, int32_t k, double* out4);
 
 #ifdef __cplusplus
 }

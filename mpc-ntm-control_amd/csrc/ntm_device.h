@@ -44,6 +44,22 @@ struct Coef {
     int rho1_sq;    // D18 switch
 };
 
+// Scenario generator (ntm_ctx_set_scenarios): per-scenario plasma parameters
+// and per-step plant disturbances, counter-based on (seed, global scenario id,
+// time index), so any sharding or batching reproduces the same realisations.
+struct Gen {
+    uint64_t seed;
+    int64_t first_id;   // global id of the launch's scenario 0
+    int k0;             // time index of the launch's first plant step
+    int dist_on;        // sigma_w or sigma_omega non-zero
+    int phys_on;        // a parameter spread non-zero
+    double sw, so;      // disturbance standard deviations (w [m], omega [rad/s])
+    double sj, sd;      // j_BS / w_dep spreads
+    // host-computed pieces of NTM_MPC_Sim.m:24,37 and B.m:2 the per-scenario
+    // C1 and b coefficient are rebuilt from (same expression order as make_prob)
+    double kTs, wsat, den, jbs, kte, wdep;
+};
+
 struct Prob {
     Coef k;
     int N, i_sim, mode, flags;
@@ -51,9 +67,54 @@ struct Prob {
     double du;        // input-rate bound (NTM_MODE_FULL_DU)
     int32_t* stats;   // optional per-scenario counters (4 x B, SoA): QP solves,
                       // GI iterations, final active rows, general (state) active rows
+    Gen g;
 };
 
 constexpr double kInf = __builtin_huge_val();
+
+// ---------------------------------------------------------------------------
+// Counter-based scenario generator (host and device share this code, so the
+// library's host-side sampler ntm_scenario_sample returns the device's values)
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+// uniform [0, 1) from (seed, global scenario id, time index k, channel ch < 256)
+__host__ __device__ __forceinline__ double gen_u01(uint64_t seed, int64_t sid, uint32_t k, uint32_t ch) {
+    uint64_t h = splitmix64(seed ^ 0xD1B54A32D192ED03ull);
+    h = splitmix64(h ^ (uint64_t)sid);
+    h = splitmix64(h ^ (((uint64_t)k << 8) | ch));
+    return (double)(h >> 11) * (1.0 / 9007199254740992.0);
+}
+// unit-variance, zero-mean Irwin-Hall(4) sample (bounded at +-2 sqrt(3)); only
+// + and * so host and device agree bit for bit.  Channel c uses sub-channels 4c..4c+3.
+__host__ __device__ __forceinline__ double gen_normal(uint64_t seed, int64_t sid, uint32_t k, uint32_t c) {
+    double s = gen_u01(seed, sid, k, 4 * c);
+    s = s + gen_u01(seed, sid, k, 4 * c + 1);
+    s = s + gen_u01(seed, sid, k, 4 * c + 2);
+    s = s + gen_u01(seed, sid, k, 4 * c + 3);
+    return (s - 2.0) * 1.7320508075688772;
+}
+constexpr uint32_t kGenParamK = 0xFFFFFFFFu;   // time index of the per-scenario parameters
+// per-scenario factor 1 + spread (2u - 1) of parameter channel c (0 j_BS, 1 w_dep)
+// (an explicit fused multiply-add: compilers may or may not contract 1 + a b, so the
+// generator fixes the rounding itself and every implementation agrees bit for bit)
+__host__ __device__ __forceinline__ double gen_factor(uint64_t seed, int64_t sid, uint32_t c, double spread) {
+    return fma(spread, 2.0 * gen_u01(seed, sid, kGenParamK, c) - 1.0, 1.0);
+}
+// scenario sid's plasma (j_BS, w_dep) into the coefficients that depend on them:
+// C1 (NTM_MPC_Sim.m:37), the B.m:2 gain and rho3's w_dep (rho3.m:2)
+__host__ __device__ __forceinline__ void gen_apply_physics(Prob& p, int64_t sid) {
+    const Gen& g = p.g;
+    const double jbs = g.jbs * gen_factor(g.seed, sid, 0, g.sj);
+    const double wdep = g.wdep * gen_factor(g.seed, sid, 1, g.sd);
+    p.k.C1 = -4.0 / 3.0 * (g.kTs * jbs * g.wsat) / g.den;
+    p.k.bc = g.kte / wdep;
+    p.k.wdep = wdep;
+}
 
 
 // 1/sqrt(x) for x > 0: v_rsq_f64 plus two Newton steps (full fp64 accuracy;
@@ -130,7 +191,7 @@ constexpr int kRepairs = 8;   // also at N = 50: 16 / 32 were no faster in mode 
 // turned a state that the plant step leaves one ulp outside a bound the
 // previous plan held it at (x_{k+1} = xmin - ulp) into an infeasible QP.
 constexpr double kConstTol = 1e-9;
-constexpr int kRowMulti = 256;     // WS::rinfo flag: the state row has two or more non-zeros        // single-row repairs of a failed warm-start candidate
+constexpr int kRowMulti = 256;     // WS::rinfo flag: the state row has two or more non-zeros
 constexpr int kGiWarmRejected = 100;   // gi_solve: the warm-start set was not dual feasible (caller reruns cold)
 
 #define NTM_WSYNC()                                              \
@@ -370,7 +431,9 @@ struct WS {
     __device__ __forceinline__ double* kdi() const { return base + oV() + 21 * n() + 3; }   // N: 1/K(k,k) (Schur)
     __device__ __forceinline__ double* ssg() const { return base + oV() + 22 * n() + 3; }   // N: sign of general row s
     __device__ __forceinline__ double* idun() const { return base + oV() + 23 * n() + 3; }  // N: 1/|D (e_i - e_{i-1})|
-    __device__ __forceinline__ int* act() const { return reinterpret_cast<int*>(base + oV() + 24 * n() + 3); }
+    // this scenario's C1, B.m gain and w_dep (scenario generator; read only when pb.g.phys_on)
+    __device__ __forceinline__ double* scn() const { return base + oV() + 24 * n() + 3; }
+    __device__ __forceinline__ int* act() const { return reinterpret_cast<int*>(base + oV() + 24 * n() + 6); }
     __device__ __forceinline__ int* sidx() const { return act() + n() + 1; }
     __device__ __forceinline__ int* cand() const { return act() + 2 * (n() + 1); }   // 2(n()+1): last two active sets
     __device__ __forceinline__ int* fidx() const { return act() + 4 * (n() + 1); }   // n()+1: free variables (polish)
@@ -383,7 +446,7 @@ struct WS {
 
 __host__ __device__ inline int ldj_of(int N) { return N | 1; }
 __host__ __device__ inline int ws_doubles(int N) {
-    return 14 * N + N * (N + 1) + (N <= kMaxNT ? 2 : 1) * N * ldj_of(N) + (N + 1) * ldj_of(N) + 24 * N + 3;
+    return 14 * N + N * (N + 1) + (N <= kMaxNT ? 2 : 1) * N * ldj_of(N) + (N + 1) * ldj_of(N) + 24 * N + 6;
 }
 // workspace bytes with room for `rows` active-row flags: the structured rows of
 // the MPC step are at most 8N+2 (getWLc 6N+4 plus 2(N-1) rate rows); a dense
@@ -401,6 +464,32 @@ __device__ inline WS<NN> ws_carve(char* base, int N) {
     w.N_rt = N;
     w.base = reinterpret_cast<double*>(base);
     return w;
+}
+
+// The scenario's LPV coefficients: the launch constants, with C1, the B.m gain and
+// w_dep taken from the workspace when the scenario generator varies the plasma
+// (written once per launch by scn_store).  Keeping the launch constants in the
+// kernel arguments matters: a copy of the whole Prob per scenario cost the N=20
+// step kernel 100 B of scratch per lane and 20 more spilled SGPRs.
+template <class W>
+__device__ __forceinline__ Coef scn_coef(const Prob& pb, const W& w) {
+    Coef k = pb.k;
+    if (pb.g.phys_on) {
+        k.C1 = w.scn()[0];
+        k.bc = w.scn()[1];
+        k.wdep = w.scn()[2];
+    }
+    return k;
+}
+template <class W>
+__device__ __forceinline__ void scn_store(const Prob& pb, const W& w, int64_t gid, int l) {
+    if (pb.g.phys_on && l == 0) {
+        Prob q = pb;
+        gen_apply_physics(q, gid);
+        w.scn()[0] = q.k.C1;
+        w.scn()[1] = q.k.bc;
+        w.scn()[2] = q.k.wdep;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -569,16 +658,79 @@ __device__ __forceinline__ void gamma_row_dot2(const W& w, int r, const double* 
 // ---------------------------------------------------------------------------
 // L2: lifted prediction  (Rho_to_PhiGammaLambda.m:17-52, CANON D4/D6)
 // ---------------------------------------------------------------------------
+// Literal-reference lift (D4 / D6; generic kernels only, the host dispatches any
+// launch that sets these flags there): D6 takes A(rho_{i-j}) for Gamma_ij, i.e.
+// the coefficient index i - j - 1 counted from 0 (Rho_to_PhiGammaLambda.m:32);
+// D4 right-multiplies Phi_i = Phi_{i-1} A_i (:21).  Same arithmetic as
+// oracle/ntm_oracle.c orc_lift.  Lane j < N runs Gamma's column j; lane 0 then
+// runs Phi and Lambda.  Kept apart from lift_phase so that the specialised hot
+// kernels compile exactly as before (folding the switches into lift_phase cost
+// the N=20 kernel 72 B of scratch per lane although they are constant there).
+template <int P, class W>
+__device__ __forceinline__ void lift_literal(const Prob& pb, const W& w, const Coef& k, int l) {
+    const int N = w.n();
+    const bool d6 = (pb.flags & NTM_LITERAL_GAMMA_INDEX) != 0, d4 = (pb.flags & NTM_LITERAL_PHI_RIGHTMUL) != 0;
+    for (int j = l; j < N; j += P) {
+        double* col = w.Gt() + w.gidx(2 * j, j) - 2 * j;
+        double g0 = w.bb()[j], g1 = 0.0;
+        col[2 * j] = g0;
+        col[2 * j + 1] = g1;
+        for (int i = j + 1; i < N; ++i) {
+            const int ai = d6 ? i - j - 1 : i;
+            const double n0 = w.a11()[ai] * g0;
+            const double n1 = w.a21()[ai] * g0 + k.a22 * g1;
+            g0 = n0;
+            g1 = n1;
+            col[2 * i] = g0;
+            col[2 * i + 1] = g1;
+        }
+    }
+    if (l == 0) {
+        double p00 = w.a11()[0], p10 = w.a21()[0], p01 = 0.0, p11 = k.a22;
+        double l0 = k.C1, l1 = k.C2;
+        w.Phi()[0] = p00; w.Phi()[1] = p10; w.Phi()[2] = p01; w.Phi()[3] = p11;
+        w.Lam()[0] = l0; w.Lam()[1] = l1;
+        for (int i = 1; i < N; ++i) {
+            const double a11 = w.a11()[i], a21 = w.a21()[i];
+            double q00, q01, q10, q11;
+            if (d4) {                                  // Phi_{i-1} A_i
+                q00 = p00 * a11 + p01 * a21;
+                q01 = p01 * k.a22;
+                q10 = p10 * a11 + p11 * a21;
+                q11 = p11 * k.a22;
+            } else {                                   // A_i Phi_{i-1}
+                q00 = a11 * p00;
+                q01 = a11 * p01;
+                q10 = a21 * p00 + k.a22 * p10;
+                q11 = a21 * p01 + k.a22 * p11;
+            }
+            p00 = q00; p01 = q01; p10 = q10; p11 = q11;
+            const double m0 = a11 * l0 + k.C1;
+            const double m1 = (a21 * l0 + k.a22 * l1) + k.C2;
+            l0 = m0; l1 = m1;
+            w.Phi()[4 * i] = p00; w.Phi()[4 * i + 1] = p10; w.Phi()[4 * i + 2] = p01; w.Phi()[4 * i + 3] = p11;
+            w.Lam()[2 * i] = l0; w.Lam()[2 * i + 1] = l1;
+        }
+    }
+    NTM_WSYNC();
+}
+
 template <int P, class W>
 __device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l) {
     const int N = w.n();
-    const Coef& k = pb.k;
+    const Coef k = scn_coef(pb, w);
     if (l < N) {
         w.a11()[l] = coef_a11(k, w.rho()[3 * l]);
         w.a21()[l] = coef_a21(k, w.rho()[3 * l + 1]);
         w.bb()[l] = coef_b(k, w.rho()[3 * l + 2]);
     }
     NTM_WSYNC();
+    if constexpr (W::kNN == 0) {
+        if (pb.flags & (NTM_LITERAL_PHI_RIGHTMUL | NTM_LITERAL_GAMMA_INDEX)) {
+            lift_literal<P>(pb, w, k, l);
+            return;
+        }
+    }
     NTM_T0(tlf);
     // Gamma: lane j owns column j: Gamma_jj = B_j, Gamma_ij = A_i Gamma_{i-1,j} (D6).
     // Lanes N and N+1 run the same 2-vector recursion for the two columns of
@@ -2487,7 +2639,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
 template <int P, class W>
 __device__ __forceinline__ bool rollout_phase(const Prob& pb, const W& w, double x0, double x1, int l) {
     const int N = w.n();
-    const Coef& k = pb.k;
+    const Coef k = scn_coef(pb, w);
     if (l == 0) {
         double y0 = x0, y1 = x1;
         w.xp()[0] = y0;
@@ -2535,16 +2687,21 @@ __device__ __forceinline__ bool rollout_phase(const Prob& pb, const W& w, double
     return conv;
 }
 
-// plant step NTM_MPC_Sim.m:130 (CANON D13: plant = prediction model, + C)
-__device__ __forceinline__ void plant_step(const Prob& pb, double x0, double x1, double u,
-                                           double& n0, double& n1) {
-    const Coef& k = pb.k;
+// plant step NTM_MPC_Sim.m:130 (CANON D13: plant = prediction model, + C), plus
+// the scenario's disturbance realisation at time index kt (ntm_ctx_set_scenarios;
+// the model the controller predicts with does not know it)
+__device__ __forceinline__ void plant_step(const Prob& pb, const Coef& k, double x0, double x1, double u,
+                                           double& n0, double& n1, int64_t gid = 0, int kt = 0) {
     double r1, r2, r3;
     rho_eval(k, x0, x1, r1, r2, r3);
     double a11 = coef_a11(k, r1), a21 = coef_a21(k, r2), b = coef_b(k, r3);
     n0 = a11 * x0 + b * u;
     n1 = a21 * x0 + k.a22 * x1;
     if (!(pb.flags & NTM_LITERAL_PLANT_NO_C)) { n0 += k.C1; n1 += k.C2; }
+    if (pb.g.dist_on) {
+        if (pb.g.sw != 0.0) n0 += pb.g.sw * gen_normal(pb.g.seed, gid, (uint32_t)kt, 0);
+        if (pb.g.so != 0.0) n1 += pb.g.so * gen_normal(pb.g.seed, gid, (uint32_t)kt, 1);
+    }
 }
 
 // ---------------------------------------------------------------------------

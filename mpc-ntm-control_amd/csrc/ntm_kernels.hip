@@ -164,6 +164,8 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, 
         w.cand()[l * (N + 1) + N] = -1;
     }
     load_state<P>(w, B, s, rho, U_old, l);
+    scn_store(pb, w, pb.g.first_id + s, l);           // this scenario's plasma (generator)
+    NTM_WSYNC();
     int its;
     int flag = mpc_step_dev<P>(pb, w, x0, x1, l, &its, B, s);
     // scenario-major outputs: each wave writes its scenario's contiguous records
@@ -173,7 +175,7 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, 
     store_record<P>(x_pred + s * (2 * (N + 1)), w.xp(), 2 * (N + 1), l);
     {
         double n0, n1;
-        plant_step(pb, x0, x1, w.U()[0], n0, n1);
+        plant_step(pb, scn_coef(pb, w), x0, x1, w.U()[0], n0, n1, pb.g.first_id + s, pb.g.k0);
         if (is16(x_next)) {
             if (l == 0) *reinterpret_cast<double2*>(x_next + 2 * s) = make_double2(n0, n1);
         } else if (l < 2) {
@@ -202,9 +204,11 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_run(Prob pb, i
     auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
     double x0 = x0v[2 * s], x1 = x0v[2 * s + 1];
     if (l < 2) w.cand()[l * (N + 1) + N] = -1;
+    scn_store(pb, w, pb.g.first_id + s, l);           // this scenario's plasma (generator)
+    NTM_WSYNC();
     {   // Rho = repmat(rho(x0), 1, N) (NTM_MPC_Sim.m:63-65); Uold = +inf (D14)
         double r1, r2, r3;
-        rho_eval(pb.k, x0, x1, r1, r2, r3);
+        rho_eval(scn_coef(pb, w), x0, x1, r1, r2, r3);
         if (l < N) {
             w.rho()[3 * l] = r1;
             w.rho()[3 * l + 1] = r2;
@@ -220,7 +224,7 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_run(Prob pb, i
         if (Uk && l < N) Uk[(s * k_sim + kk) * N + l] = w.U()[l];
         if (wpred) for (int i = l; i <= N; i += P) wpred[(s * k_sim + kk) * (N + 1) + i] = w.xp()[2 * i];
         double n0, n1;
-        plant_step(pb, x0, x1, w.U()[0], n0, n1);
+        plant_step(pb, scn_coef(pb, w), x0, x1, w.U()[0], n0, n1, pb.g.first_id + s, pb.g.k0 + kk);
         if (l == 0) {
             if (uk) uk[s * k_sim + kk] = w.U()[0];
             if (exitflag) exitflag[s * k_sim + kk] = flag;
@@ -248,8 +252,10 @@ __global__ void k_rho(Prob pb, int64_t B, const double* x, double* rho) {
 __global__ void k_init_state(Prob pb, int64_t B, const double* x, double* rho, double* U_old) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= B) return;
+    Prob pbs = pb;                                     // scenario's w_dep (rho3.m:2)
+    if (pb.g.phys_on) gen_apply_physics(pbs, pb.g.first_id + s);
     double r1, r2, r3;
-    rho_eval(pb.k, x[2 * s], x[2 * s + 1], r1, r2, r3);
+    rho_eval(pbs.k, x[2 * s], x[2 * s + 1], r1, r2, r3);
     double* rs = rho + s * (3 * pb.N);
     for (int i = 0; i < pb.N; ++i) {
         rs[3 * i] = r1;
@@ -427,10 +433,15 @@ __global__ __launch_bounds__(64) void k_qp(int64_t B, int N, int m, const double
 }
 
 // ------------------------------------------------------------------ host helpers
+// NTM_MPC_Sim.m:24 (same expression as oracle/ntm_oracle.c orc_coeffs)
+double kappa_of(const ntm_physics* p) {
+    const double pi = 3.14159265358979323846;
+    return 16 * p->mu0 * p->Lq * (p->rs * p->rs) / (0.82 * p->tau_r * p->B_pol * pi);
+}
+
 Prob make_prob(const ntm_physics* p, const ntm_config* c) {
     // identical expressions to oracle/ntm_oracle.c orc_coeffs (NTM_MPC_Sim.m:24-25, 37; A.m; B.m)
-    const double pi = 3.14159265358979323846;
-    double kappa = 16 * p->mu0 * p->Lq * (p->rs * p->rs) / (0.82 * p->tau_r * p->B_pol * pi);
+    double kappa = kappa_of(p);
     double zeta = p->m * p->Cw * (p->tau_A0 * p->tau_A0) * p->tau_w * (p->a * p->a * p->a);
     Prob pb;
     std::memset(&pb, 0, sizeof(pb));
@@ -462,6 +473,27 @@ Prob make_prob(const ntm_physics* p, const ntm_config* c) {
     return pb;
 }
 
+// a scenario generator into pb.g (the time-step entry points); the pieces of
+// C1 (NTM_MPC_Sim.m:37) and of the B.m:2 gain that gen_apply_physics rebuilds
+// per scenario, in make_prob's expression order
+void attach_gen(const ntm_scenario_gen& g, const ntm_physics* p, const ntm_config* c, Prob& pb) {
+    pb.g.seed = g.seed;
+    pb.g.first_id = g.first_id;
+    pb.g.k0 = g.k0;
+    pb.g.sw = g.sigma_w;
+    pb.g.so = g.sigma_omega;
+    pb.g.dist_on = (g.sigma_w != 0.0 || g.sigma_omega != 0.0) ? 1 : 0;
+    pb.g.sj = g.jbs_spread;
+    pb.g.sd = g.wdep_spread;
+    pb.g.phys_on = (g.jbs_spread != 0.0 || g.wdep_spread != 0.0) ? 1 : 0;
+    pb.g.kTs = kappa_of(p) * c->Ts;
+    pb.g.wsat = p->w_sat;
+    pb.g.den = p->w_sat * p->w_sat + p->w_marg * p->w_marg;
+    pb.g.jbs = p->j_BS;
+    pb.g.kte = pb.g.kTs * p->eta_CD;
+    pb.g.wdep = p->w_dep;
+}
+
 int lanes_for(int N) {
     // lanes per scenario: the smallest power of two >= N (NTM_LANES=64 forces one scenario per wave)
     static int forced = [] {
@@ -483,6 +515,8 @@ int lanes_for(int N) {
 struct ntm_ctx {
     int device = 0;
     int32_t* stats = nullptr;   // optional device counters (ntm_ctx_set_stats)
+    bool gen_on = false;        // scenario generator attached (ntm_ctx_set_scenarios)
+    ntm_scenario_gen gen{};
     std::string err;
     void* dbuf = nullptr;
     size_t dbuf_bytes = 0;
@@ -518,11 +552,17 @@ int check_hip(ntm_ctx* ctx, hipError_t e, const char* what) {
     return fail(ctx, NTM_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+constexpr int kKnownFlags =
+    NTM_LITERAL_PHI_RIGHTMUL | NTM_LITERAL_GAMMA_INDEX | NTM_LITERAL_PLANT_NO_C | NTM_RHO1_SQUARED;
+// D4 / D6 are compiled into the generic (runtime-N) kernels only
+constexpr int kGenericOnlyFlags = NTM_LITERAL_PHI_RIGHTMUL | NTM_LITERAL_GAMMA_INDEX;
+
 int validate(ntm_ctx* ctx, const ntm_physics* p, const ntm_config* c, int64_t B) {
     if (!ctx) return NTM_E_INVALID;
     if (!p || !c) return fail(ctx, NTM_E_INVALID, "null physics/config");
     if (c->N < 1 || c->N > NTM_MAX_N) return fail(ctx, NTM_E_INVALID, "N out of range [1, 64]");
     if (c->i_sim < 1) return fail(ctx, NTM_E_INVALID, "i_sim must be >= 1");
+    if (c->flags & ~kKnownFlags) return fail(ctx, NTM_E_UNSUPPORTED, "unknown flag bits");
     if (c->mode < NTM_MODE_NONE || c->mode > NTM_MODE_FULL_DU) return fail(ctx, NTM_E_INVALID, "bad mode");
     if (c->mode == NTM_MODE_FULL_DU && !(std::isfinite(c->du_max)))
         return fail(ctx, NTM_E_INVALID, "du_max must be finite");
@@ -579,13 +619,14 @@ bool force_generic() {
     static bool g = std::getenv("NTM_GENERIC") != nullptr;
     return g;
 }
+bool use_generic(int flags) { return force_generic() || (flags & kGenericOnlyFlags) != 0; }
 #ifdef NTM_RU_ONLY20
 // resource-usage check of the N=20 hot kernel alone (make ru20): every horizon
 // goes to it; the library built this way is not for use
-#define NTM_DISPATCH_P(N, CALL) CALL(64, 20)
+#define NTM_DISPATCH_P(N, GEN, CALL) CALL(64, 20)
 #else
-#define NTM_DISPATCH_P(N, CALL)                                                     \
-    (force_generic() ? (lanes_for(N) == 16 ? CALL(16, 0) : (lanes_for(N) == 32 ? CALL(32, 0) : CALL(64, 0))) \
+#define NTM_DISPATCH_P(N, GEN, CALL)                                                \
+    ((GEN) ? (lanes_for(N) == 16 ? CALL(16, 0) : (lanes_for(N) == 32 ? CALL(32, 0) : CALL(64, 0))) \
     : lanes_for(N) == 16 ? ((N) == 10 ? CALL(16, 10) : CALL(16, 0))                  \
                         : (lanes_for(N) == 32 ? CALL(32, 0)                          \
                                               : ((N) == 20 ? CALL(64, 20)            \
@@ -667,12 +708,21 @@ int ntm_ctx_create(ntm_ctx** out, int32_t device) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return NTM_E_DEVICE;
     if (device < 0 || device >= n) return NTM_E_INVALID;
-    if (hipSetDevice(device) != hipSuccess) return NTM_E_DEVICE;
     ntm_ctx* c = new ntm_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    int rc = NTM_OK;
+    {
+        // the stream is created on ctx->device; the guard restores the caller's
+        // current device on every path out of this block
+        DeviceGuard dg(c);
+        int cur = -1;
+        if (hipGetDevice(&cur) != hipSuccess || cur != device ||
+            hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+            rc = NTM_E_DEVICE;
+    }
+    if (rc != NTM_OK) {
         delete c;
-        return NTM_E_DEVICE;
+        return rc;
     }
     *out = c;
     return NTM_OK;
@@ -712,6 +762,35 @@ int ntm_ctx_set_stats(ntm_ctx* ctx, int32_t* dev_stats) {
     return NTM_OK;
 }
 
+int ntm_ctx_set_scenarios(ntm_ctx* ctx, const ntm_scenario_gen* gen) {
+    if (!ctx) return NTM_E_INVALID;
+    if (!gen) {
+        ctx->gen_on = false;
+        return NTM_OK;
+    }
+    const double v[4] = {gen->sigma_w, gen->sigma_omega, gen->jbs_spread, gen->wdep_spread};
+    for (double x : v)
+        if (!std::isfinite(x) || x < 0.0) return fail(ctx, NTM_E_INVALID, "generator parameters must be finite and >= 0");
+    if (gen->jbs_spread >= 1.0 || gen->wdep_spread >= 1.0)
+        return fail(ctx, NTM_E_INVALID, "parameter spreads must be < 1");
+    if (gen->reserved != 0) return fail(ctx, NTM_E_INVALID, "reserved must be 0");
+    if (gen->k0 < 0) return fail(ctx, NTM_E_INVALID, "negative k0");
+    ctx->gen = *gen;
+    ctx->gen_on = true;
+    return NTM_OK;
+}
+
+void ntm_scenario_sample(const ntm_scenario_gen* gen, int64_t B, int32_t k, double* out4) {
+    // the device's own generator code (ntm_device.h), compiled for the host
+    for (int64_t s = 0; s < B; ++s) {
+        const int64_t id = gen->first_id + s;
+        out4[4 * s] = gen_factor(gen->seed, id, 0, gen->jbs_spread);
+        out4[4 * s + 1] = gen_factor(gen->seed, id, 1, gen->wdep_spread);
+        out4[4 * s + 2] = gen_normal(gen->seed, id, (uint32_t)k, 0);
+        out4[4 * s + 3] = gen_normal(gen->seed, id, (uint32_t)k, 1);
+    }
+}
+
 int ntm_mpc_step_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* cfg, int64_t B,
                         const double* x_k, double* rho, double* U_old, double* U, double* x_pred, double* x_next,
                         int32_t* exitflag, int32_t* inner_iters, void* stream) {
@@ -730,17 +809,18 @@ int ntm_mpc_step_ws_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_conf
         return fail(ctx, NTM_E_INVALID, "null array");
     Prob pb = make_prob(phys, cfg);
     pb.stats = ctx->stats;
+    if (ctx->gen_on) attach_gen(ctx->gen, phys, cfg, pb);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define CALL(P, NN) \
     launch_step<P, NN>(ctx, pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, active_ws, st)
-    return NTM_DISPATCH_P(cfg->N, CALL);
+    return NTM_DISPATCH_P(cfg->N, use_generic(cfg->flags), CALL);
 #undef CALL
 }
 
 int ntm_step_launch_info(int32_t N, int32_t* lanes, int32_t* horizon_template) {
     if (N < 1 || N > NTM_MAX_N || !lanes || !horizon_template) return NTM_E_INVALID;
 #define INFO(P_, NN_) (*lanes = (P_), *horizon_template = (NN_), 0)
-    return NTM_DISPATCH_P(N, INFO);
+    return NTM_DISPATCH_P(N, force_generic(), INFO);
 #undef INFO
 }
 
@@ -807,9 +887,10 @@ int ntm_mpc_run_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* 
     if (!x0) return fail(ctx, NTM_E_INVALID, "null x0");
     Prob pb = make_prob(phys, cfg);
     pb.stats = ctx->stats;
+    if (ctx->gen_on) attach_gen(ctx->gen, phys, cfg, pb);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define CALL(P, NN) launch_run<P, NN>(ctx, pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, st)
-    return NTM_DISPATCH_P(cfg->N, CALL);
+    return NTM_DISPATCH_P(cfg->N, use_generic(cfg->flags), CALL);
 #undef CALL
 }
 
@@ -868,6 +949,7 @@ int ntm_mpc_init_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config*
     if (rc || B == 0) return rc;
     if (!x0 || !rho || !U_old) return fail(ctx, NTM_E_INVALID, "null array");
     Prob pb = make_prob(phys, cfg);
+    if (ctx->gen_on) attach_gen(ctx->gen, phys, cfg, pb);
     hipLaunchKernelGGL(k_init_state, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, (hipStream_t)stream, pb, B,
                        x0, rho, U_old);
     return check_hip(ctx, hipGetLastError(), "k_init_state");
@@ -983,13 +1065,6 @@ int ntm_qp_device(ntm_ctx* ctx, int64_t B, int32_t N, int32_t m, const double* G
 }
 
 // splitmix64-based counter generator (identical to oracle/ntm_oracle.py scenario_x0)
-static uint64_t splitmix64(uint64_t z) {
-    z += 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
 void ntm_scenarios_x0(uint64_t seed, int64_t first_id, int64_t B, double* x0) {
     const double pi = 3.14159265358979323846;
     for (int64_t k = 0; k < B; ++k) {

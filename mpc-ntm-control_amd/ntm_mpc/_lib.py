@@ -14,7 +14,7 @@ LIB_PATH = Path(os.environ.get("NTM_MPC_LIB", PKG_ROOT / "lib" / "libntm_mpc.so"
 
 MAX_N = 64
 MODE_NONE, MODE_BOX, MODE_FULL, MODE_FULL_DU = 0, 1, 2, 3
-ABI_VERSION = 3          # include/ntm_mpc.h NTM_MPC_ABI_VERSION
+ABI_VERSION = 4          # include/ntm_mpc.h NTM_MPC_ABI_VERSION
 LITERAL_PHI_RIGHTMUL, LITERAL_GAMMA_INDEX, LITERAL_PLANT_NO_C, RHO1_SQUARED = 1, 2, 4, 8
 EXIT_OPTIMAL, EXIT_MAXITER, EXIT_INFEASIBLE, EXIT_NONFINITE = 1, 0, -2, -7
 NTM_OK = 0
@@ -38,6 +38,13 @@ class NtmConfig(C.Structure):
                 ("Ts", C.c_double), ("xmin", C.c_double * 2), ("xmax", C.c_double * 2),
                 ("umin", C.c_double), ("umax", C.c_double), ("Q", C.c_double * 4),
                 ("r", C.c_double * 2), ("epsilon", C.c_double), ("du_max", C.c_double)]
+
+
+class NtmScenarioGen(C.Structure):
+    """ntm_scenario_gen — plasma scenarios and disturbance realisations (include/ntm_mpc.h)."""
+    _fields_ = [("seed", C.c_uint64), ("first_id", C.c_int64), ("k0", C.c_int32), ("reserved", C.c_int32),
+                ("sigma_w", C.c_double), ("sigma_omega", C.c_double), ("jbs_spread", C.c_double),
+                ("wdep_spread", C.c_double)]
 
 
 _DP = C.POINTER(C.c_double)
@@ -74,6 +81,8 @@ EXPORTS = {
     "ntm_getwlc_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _V, _V, _V, _V, _V]),
     "ntm_qp_device": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, _V, _V, _V, _V, _V, _V, _V, _V]),
     "ntm_scenarios_x0": (None, [C.c_uint64, C.c_int64, C.c_int64, _DP]),
+    "ntm_ctx_set_scenarios": (C.c_int, [C.c_void_p, C.POINTER(NtmScenarioGen)]),
+    "ntm_scenario_sample": (None, [C.POINTER(NtmScenarioGen), C.c_int64, C.c_int32, _DP]),
 }
 
 _lib = None

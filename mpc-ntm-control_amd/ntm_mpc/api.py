@@ -28,6 +28,7 @@ fallback: without the library or a GPU, calls raise.
 from __future__ import annotations
 
 import ctypes as C
+import dataclasses
 import math
 from dataclasses import dataclass
 
@@ -35,7 +36,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
-from ._lib import NtmConfig, NtmLibraryError, NtmPhysics
+from ._lib import NtmConfig, NtmLibraryError, NtmPhysics, NtmScenarioGen
 
 
 STATS_ROWS = 6   # include/ntm_mpc.h NTM_STATS_ROWS
@@ -97,6 +98,34 @@ class Config:
         if self.mode == L.MODE_BOX:
             return 2 * self.N
         return 6 * self.N + 4 + (2 * (self.N - 1) if self.mode == L.MODE_FULL_DU else 0)
+
+
+@dataclass
+class ScenarioGen:
+    """ntm_scenario_gen: independent plasma scenarios (j_BS, w_dep of NTM_MPC_Sim.m:5-6,
+    each scaled by 1 + spread (2u - 1)) and additive plant disturbances (on
+    NTM_MPC_Sim.m:130, unit-variance Irwin-Hall samples times sigma), all
+    counter-based on (seed, global scenario id, time index)."""
+    seed: int = 20241220
+    first_id: int = 0          # global id of the batch's scenario 0 (a shard's offset)
+    k0: int = 0                # time index of the next launch's first plant step
+    sigma_w: float = 0.0       # [m]
+    sigma_omega: float = 0.0   # [rad/s]
+    jbs_spread: float = 0.0
+    wdep_spread: float = 0.0
+
+    def to_c(self) -> NtmScenarioGen:
+        return NtmScenarioGen(int(self.seed) & 0xFFFFFFFFFFFFFFFF, int(self.first_id), int(self.k0), 0,
+                              float(self.sigma_w), float(self.sigma_omega), float(self.jbs_spread),
+                              float(self.wdep_spread))
+
+
+def scenario_sample(gen: ScenarioGen, B: int, k: int = 0) -> np.ndarray:
+    """(B, 4) host-side samples of the generator for scenarios gen.first_id + s: j_BS
+    factor, w_dep factor, n_w(k), n_omega(k) (ntm_scenario_sample; no GPU needed)."""
+    out = np.zeros((B, 4))
+    L.load().ntm_scenario_sample(C.byref(gen.to_c()), B, k, out.ctypes.data_as(C.POINTER(C.c_double)))
+    return out
 
 
 def _ptr(t: torch.Tensor | None):
@@ -169,6 +198,7 @@ class NtmMpc:
         self.device = torch.cuda.current_device() if device is None else int(device)
         self.physics = physics or Physics()
         self.config = config or Config()
+        self.gen = None
         self._ctx = C.c_void_p()
         rc = self.lib.ntm_ctx_create(C.byref(self._ctx), self.device)
         if rc != L.NTM_OK:
@@ -217,6 +247,15 @@ class NtmMpc:
                 raise ValueError(f"stats must be ({STATS_ROWS}, B) int32")
             _check_dev(stats, tuple(stats.shape), dtype=torch.int32, name="stats")
         self._raise(self.lib.ntm_ctx_set_stats(self._ctx, _ptr(stats)), "ntm_ctx_set_stats")
+
+    def set_scenarios(self, gen: ScenarioGen | None):
+        """Attach a scenario generator (ntm_ctx_set_scenarios): subsequent
+        initial_state / step / run launches use each scenario's own plasma and
+        add its disturbance realisation to the plant step; None restores the
+        nominal, disturbance-free loop of the reference."""
+        self.gen = gen
+        self._raise(self.lib.ntm_ctx_set_scenarios(self._ctx, None if gen is None else C.byref(gen.to_c())),
+                    "ntm_ctx_set_scenarios")
 
     def step_kernel_name(self, B: int, cfg: Config | None = None) -> str:
         """Name of the fused step kernel specialisation a launch uses (reporting)."""
@@ -345,12 +384,13 @@ class NtmMpc:
         return out
 
     # ------------------------------------------------------------ function level
-    def rho(self, x: torch.Tensor, cfg: Config | None = None):
-        """rho1.m / rho2.m / rho3.m at x (2, B) -> (3, B)."""
+    def rho(self, x: torch.Tensor, cfg: Config | None = None, physics: Physics | None = None):
+        """rho1.m / rho2.m / rho3.m at x (2, B) -> (3, B) (``physics`` overrides w_marg / w_dep)."""
         Bn = x.shape[1]
         x, _ = _dev_arg(x, (2, Bn), name="x")
         out = self._empty(3, Bn)
-        self._raise(self.lib.ntm_rho_device(self._ctx, C.byref(self.physics.to_c()), C.byref(self._cfg(cfg)), Bn,
+        ph = physics or self.physics
+        self._raise(self.lib.ntm_rho_device(self._ctx, C.byref(ph.to_c()), C.byref(self._cfg(cfg)), Bn,
                                             _ptr(x), _ptr(out), self._stream()), "ntm_rho_device")
         return out
 
@@ -439,19 +479,26 @@ def _ctl():
     return _default
 
 
-def rho1(x, w_marg=None):
-    """rho1.m (batched): x (2, B) CUDA -> (B,)."""
-    return _ctl().rho(x)[0]
+def _phys_with(**kw):
+    ph = _ctl().physics
+    kw = {k: float(v) for k, v in kw.items() if v is not None}
+    return dataclasses.replace(ph, **kw) if kw else ph
+
+
+def rho1(x, wmarg=None):
+    """rho1.m (batched): rho1(x, wmarg) = 1/(x(1) + wmarg^2), x (2, B) CUDA -> (B,).
+    ``wmarg`` defaults to the controller's physics (NTM_MPC_Sim.m:7)."""
+    return _ctl().rho(x, physics=_phys_with(w_marg=wmarg))[0]
 
 
 def rho2(x):
-    """rho2.m (batched)."""
+    """rho2.m (batched): x(1)^2 / x(2)."""
     return _ctl().rho(x)[1]
 
 
 def rho3(x, w_dep=None):
-    """rho3.m (batched)."""
-    return _ctl().rho(x)[2]
+    """rho3.m (batched): rho3(x, w_dep); ``w_dep`` defaults to the controller's physics (:6)."""
+    return _ctl().rho(x, physics=_phys_with(w_dep=w_dep))[2]
 
 
 def Rho_to_PhiGammaLambda(Rho1, Rho2, Rho3, cfg: Config | None = None):

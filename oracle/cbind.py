@@ -32,6 +32,18 @@ class CCfg(C.Structure):
                 ("r", C.c_double * 2), ("epsilon", C.c_double), ("du_max", C.c_double)]
 
 
+class CGen(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("first_id", C.c_int64), ("k0", C.c_int32), ("reserved", C.c_int32),
+                ("sigma_w", C.c_double), ("sigma_omega", C.c_double), ("jbs_spread", C.c_double),
+                ("wdep_spread", C.c_double)]
+
+
+def gen_c(g: "O.ScenarioGen | None"):
+    if g is None:
+        return None
+    return C.byref(CGen(g.seed, g.first_id, g.k0, 0, g.sigma_w, g.sigma_omega, g.jbs_spread, g.wdep_spread))
+
+
 def build():
     subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
 
@@ -67,23 +79,25 @@ def _ip(a):
     return a.ctypes.data_as(C.POINTER(C.c_int32)) if a is not None else None
 
 
-def run(x0, cfg: O.Config, k_sim: int, ph: O.Physics | None = None, nthreads: int = 0):
-    """Closed loop (NTM_MPC_Sim.m:80-131) for x0 (2, B).  Same output layout as ntm_mpc_run."""
+def run(x0, cfg: O.Config, k_sim: int, ph: O.Physics | None = None, nthreads: int = 0, gen=None):
+    """Closed loop (NTM_MPC_Sim.m:80-131) for x0 (2, B).  Same output layout as ntm_mpc_run;
+    ``gen`` (O.ScenarioGen) adds the scenario generator."""
     x0 = np.ascontiguousarray(x0, dtype=np.float64)
     B = x0.shape[1]
     N = cfg.N
     out = {"xk": np.zeros((2 * (k_sim + 1), B)), "uk": np.zeros((k_sim, B)), "Uk": np.zeros((N * k_sim, B)),
            "wpred": np.zeros(((N + 1) * k_sim, B)), "exitflag": np.zeros((k_sim, B), np.int32),
            "inner_iters": np.zeros((k_sim, B), np.int32)}
-    rc = lib().ntm_oracle_run(C.byref(phys_c(ph)), C.byref(cfg_c(cfg)), C.c_int64(B), k_sim, _dp(x0),
-                              _dp(out["xk"]), _dp(out["uk"]), _dp(out["Uk"]), _dp(out["wpred"]),
-                              _ip(out["exitflag"]), _ip(out["inner_iters"]), nthreads)
+    rc = lib().ntm_oracle_run_gen(C.byref(phys_c(ph)), C.byref(cfg_c(cfg)), gen_c(gen), C.c_int64(B), k_sim,
+                                  _dp(x0), _dp(out["xk"]), _dp(out["uk"]), _dp(out["Uk"]), _dp(out["wpred"]),
+                                  _ip(out["exitflag"]), _ip(out["inner_iters"]), nthreads)
     assert rc == 0, rc
     return out
 
 
-def step(x_k, rho, U_old, cfg: O.Config, ph: O.Physics | None = None, nthreads: int = 0):
-    """One MPC step (NTM_MPC_Sim.m:94-130) for a batch; rho / U_old are copied, not modified."""
+def step(x_k, rho, U_old, cfg: O.Config, ph: O.Physics | None = None, nthreads: int = 0, gen=None):
+    """One MPC step (NTM_MPC_Sim.m:94-130) for a batch; rho / U_old are copied, not modified.
+    ``gen`` (O.ScenarioGen) adds the scenario generator (plant step at time index gen.k0)."""
     x_k = np.ascontiguousarray(x_k, dtype=np.float64)
     rho = np.array(rho, dtype=np.float64, order="C")
     U_old = np.array(U_old, dtype=np.float64, order="C")
@@ -91,9 +105,9 @@ def step(x_k, rho, U_old, cfg: O.Config, ph: O.Physics | None = None, nthreads: 
     N = cfg.N
     out = {"U": np.zeros((N, B)), "x_pred": np.zeros((2 * (N + 1), B)), "x_next": np.zeros((2, B)),
            "exitflag": np.zeros(B, np.int32), "inner_iters": np.zeros(B, np.int32)}
-    rc = lib().ntm_oracle_step(C.byref(phys_c(ph)), C.byref(cfg_c(cfg)), C.c_int64(B), _dp(x_k), _dp(rho),
-                               _dp(U_old), _dp(out["U"]), _dp(out["x_pred"]), _dp(out["x_next"]),
-                               _ip(out["exitflag"]), _ip(out["inner_iters"]), nthreads)
+    rc = lib().ntm_oracle_step_gen(C.byref(phys_c(ph)), C.byref(cfg_c(cfg)), gen_c(gen), C.c_int64(B), _dp(x_k),
+                                   _dp(rho), _dp(U_old), _dp(out["U"]), _dp(out["x_pred"]), _dp(out["x_next"]),
+                                   _ip(out["exitflag"]), _ip(out["inner_iters"]), nthreads)
     assert rc == 0, rc
     out["rho"] = rho
     out["U_old"] = U_old
@@ -123,3 +137,22 @@ def initial_state(x0, cfg: O.Config, ph: O.Physics | None = None):
         r = O.rho_all(x0[:, s], ph, cfg)
         rho[:, s] = np.tile(r, cfg.N)
     return rho, np.full((cfg.N, B), np.inf)
+
+
+def initial_state_gen(x0, cfg: O.Config, gen=None, ph: O.Physics | None = None):
+    """ntm_oracle_init_gen: rho (3N, B) of each scenario's own plasma and U_old = +inf."""
+    x0 = np.ascontiguousarray(x0, dtype=np.float64)
+    B = x0.shape[1]
+    rho = np.zeros((3 * cfg.N, B))
+    U_old = np.zeros((cfg.N, B))
+    rc = lib().ntm_oracle_init_gen(C.byref(phys_c(ph)), C.byref(cfg_c(cfg)), gen_c(gen), C.c_int64(B), _dp(x0),
+                                   _dp(rho), _dp(U_old))
+    assert rc == 0, rc
+    return rho, U_old
+
+
+def scenario_sample(gen, B: int, k: int):
+    """(B, 4) samples of the generator: j_BS factor, w_dep factor, n_w(k), n_omega(k)."""
+    out = np.zeros((B, 4))
+    lib().ntm_oracle_scenario_sample(gen_c(gen), C.c_int64(B), C.c_int32(k), _dp(out))
+    return out

@@ -71,6 +71,45 @@ static inline double orc_a11(const orc_coef* k, double r1) { return k->a11c * r1
 static inline double orc_a21(const orc_coef* k, double r2, double Ts) { return (r2 * Ts) / k->a21num_den; }
 static inline double orc_b(const orc_coef* k, double r3) { return k->bc * r3; }
 
+/* ------------------------------------------------------------------ */
+/* Scenario generator (include/ntm_mpc.h ntm_scenario_gen): per-scenario */
+/* plasma (j_BS, w_dep; NTM_MPC_Sim.m:5-6) and plant disturbances (:130) */
+/* ------------------------------------------------------------------ */
+static uint64_t o_splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static double o_u01(uint64_t seed, int64_t id, uint32_t k, uint32_t ch) {
+    uint64_t h = o_splitmix64(seed ^ 0xD1B54A32D192ED03ull);
+    h = o_splitmix64(h ^ (uint64_t)id);
+    h = o_splitmix64(h ^ (((uint64_t)k << 8) | ch));
+    return (double)(h >> 11) * (1.0 / 9007199254740992.0);
+}
+static double o_normal(uint64_t seed, int64_t id, uint32_t k, uint32_t c) {   /* Irwin-Hall(4), unit variance */
+    double s = o_u01(seed, id, k, 4 * c);
+    s = s + o_u01(seed, id, k, 4 * c + 1);
+    s = s + o_u01(seed, id, k, 4 * c + 2);
+    s = s + o_u01(seed, id, k, 4 * c + 3);
+    return (s - 2.0) * 1.7320508075688772;
+}
+static double o_factor(uint64_t seed, int64_t id, uint32_t c, double spread) {
+    return fma(spread, 2.0 * o_u01(seed, id, 0xFFFFFFFFu, c) - 1.0, 1.0);   /* one rounding, as the device */
+}
+/* scenario id's physics: j_BS and w_dep scaled (the rest nominal) */
+static void orc_scn_physics(const ntm_physics* p, const ntm_scenario_gen* g, int64_t id, ntm_physics* ps) {
+    *ps = *p;
+    if (!g) return;
+    ps->j_BS = p->j_BS * o_factor(g->seed, id, 0, g->jbs_spread);
+    ps->w_dep = p->w_dep * o_factor(g->seed, id, 1, g->wdep_spread);
+}
+/* additive plant disturbance of scenario id at time index k */
+static void orc_disturbance(const ntm_scenario_gen* g, int64_t id, int32_t k, double* d) {
+    d[0] = (g && g->sigma_w != 0.0) ? g->sigma_w * o_normal(g->seed, id, (uint32_t)k, 0) : 0.0;
+    d[1] = (g && g->sigma_omega != 0.0) ? g->sigma_omega * o_normal(g->seed, id, (uint32_t)k, 1) : 0.0;
+}
+
 /* Rho_to_PhiGammaLambda.m:1-54 (CANON D3-D6).  rho: 3xN col-major.
  * Phi 2N x 2, Gamma 2N x N, Lambda 2N, all column-major. */
 static void orc_lift(const orc_coef* k, const ntm_config* c, const double* rho,
@@ -624,7 +663,7 @@ static int orc_solve(const orc_coef* k, const ntm_config* c, const double* rho,
 /* One MPC step, NTM_MPC_Sim.m:94-130 (CANON ordering). */
 static void orc_step(const orc_coef* k, const ntm_config* c, const double* x,
                      double* rho, double* Uold, double* U, double* xpred,
-                     double* xnext, int* flag_out, int* iters_out) {
+                     double* xnext, int* flag_out, int* iters_out, const double* dist) {
     int N = c->N;
     int flag = NTM_EXIT_OPTIMAL, it = 0;
     for (it = 1; it <= c->i_sim; ++it) {
@@ -657,6 +696,10 @@ static void orc_step(const orc_coef* k, const ntm_config* c, const double* x,
     xnext[0] = a11 * x[0] + b * U[0];
     xnext[1] = a21 * x[0] + k->a22 * x[1];
     if (!(c->flags & NTM_LITERAL_PLANT_NO_C)) { xnext[0] += k->C1; xnext[1] += k->C2; }
+    if (dist) {                                              /* scenario generator */
+        if (dist[0] != 0.0) xnext[0] += dist[0];
+        if (dist[1] != 0.0) xnext[1] += dist[1];
+    }
     *flag_out = flag;
     *iters_out = it;
 }
@@ -702,25 +745,54 @@ EXPORT int ntm_oracle_qp(int n, int m, const double* G, const double* F, const d
     return orc_qp(n, m, G, F, Lin, b, U, iters);
 }
 
-/* Batched MPC step, SoA scenario-minor layout (see include/ntm_mpc.h). */
-EXPORT int ntm_oracle_step(const ntm_physics* p, const ntm_config* c, int64_t B,
-                           const double* x_k, double* rho, double* U_old, double* U,
-                           double* x_pred, double* x_next, int32_t* exitflag,
-                           int32_t* inner_iters, int nthreads) {
+/* Per-scenario coefficients: nominal, or scenario (first_id + s)'s plasma. */
+static void orc_scn_coeffs(const ntm_physics* p, const ntm_config* c, const ntm_scenario_gen* g,
+                           int64_t s, const orc_coef* nominal, orc_coef* k) {
+    if (!g || (g->jbs_spread == 0.0 && g->wdep_spread == 0.0)) { *k = *nominal; return; }
+    ntm_physics ps;
+    orc_scn_physics(p, g, g->first_id + s, &ps);
+    orc_coeffs(&ps, c, k);
+}
+
+/* Initial LPV state (NTM_MPC_Sim.m:63-65, D14), SoA scenario-minor layout. */
+EXPORT int ntm_oracle_init_gen(const ntm_physics* p, const ntm_config* c, const ntm_scenario_gen* gen,
+                               int64_t B, const double* x0, double* rho, double* U_old) {
     if (!valid(c) || B < 0) return NTM_E_INVALID;
-    orc_coef k; orc_coeffs(p, c, &k);
+    orc_coef k0; orc_coeffs(p, c, &k0);
+    int N = c->N;
+    for (int64_t s = 0; s < B; ++s) {
+        orc_coef k; orc_scn_coeffs(p, c, gen, s, &k0, &k);
+        double x[2] = {x0[s], x0[B + s]}, r[3];
+        orc_rho(&k, x, r);
+        for (int i = 0; i < N; ++i)
+            for (int e = 0; e < 3; ++e) rho[(int64_t)(3 * i + e) * B + s] = r[e];
+        for (int j = 0; j < N; ++j) U_old[(int64_t)j * B + s] = INFINITY;
+    }
+    return 0;
+}
+
+/* Batched MPC step, SoA scenario-minor layout (see include/ntm_mpc.h); gen may be
+ * NULL (nominal plant), its k0 is the plant step's time index. */
+EXPORT int ntm_oracle_step_gen(const ntm_physics* p, const ntm_config* c, const ntm_scenario_gen* gen,
+                               int64_t B, const double* x_k, double* rho, double* U_old, double* U,
+                               double* x_pred, double* x_next, int32_t* exitflag,
+                               int32_t* inner_iters, int nthreads) {
+    if (!valid(c) || B < 0) return NTM_E_INVALID;
+    orc_coef k0; orc_coeffs(p, c, &k0);
     int N = c->N;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #pragma omp parallel for schedule(dynamic, 16)
 #endif
     for (int64_t s = 0; s < B; ++s) {
-        double x[2], rh[3 * NMAX], uo[NMAX], u[NMAX], xp[2 * (NMAX + 1)], xn[2];
+        double x[2], rh[3 * NMAX], uo[NMAX], u[NMAX], xp[2 * (NMAX + 1)], xn[2], d[2];
         int fl, its;
+        orc_coef k; orc_scn_coeffs(p, c, gen, s, &k0, &k);
+        if (gen) orc_disturbance(gen, gen->first_id + s, gen->k0, d);
         for (int e = 0; e < 2; ++e) x[e] = x_k[e * B + s];
         for (int e = 0; e < 3 * N; ++e) rh[e] = rho[e * B + s];
         for (int e = 0; e < N; ++e) uo[e] = U_old[e * B + s];
-        orc_step(&k, c, x, rh, uo, u, xp, xn, &fl, &its);
+        orc_step(&k, c, x, rh, uo, u, xp, xn, &fl, &its, gen ? d : NULL);
         for (int e = 0; e < 3 * N; ++e) rho[e * B + s] = rh[e];
         for (int e = 0; e < N; ++e) { U_old[e * B + s] = uo[e]; U[e * B + s] = u[e]; }
         for (int e = 0; e < 2 * (N + 1); ++e) x_pred[e * B + s] = xp[e];
@@ -731,19 +803,29 @@ EXPORT int ntm_oracle_step(const ntm_physics* p, const ntm_config* c, int64_t B,
     return 0;
 }
 
-/* Batched closed loop NTM_MPC_Sim.m:80-131.  Output layouts as ntm_mpc_run. */
-EXPORT int ntm_oracle_run(const ntm_physics* p, const ntm_config* c, int64_t B, int32_t k_sim,
-                          const double* x0, double* xk, double* uk, double* Uk, double* wpred,
-                          int32_t* exitflag, int32_t* inner_iters, int nthreads) {
+EXPORT int ntm_oracle_step(const ntm_physics* p, const ntm_config* c, int64_t B,
+                           const double* x_k, double* rho, double* U_old, double* U,
+                           double* x_pred, double* x_next, int32_t* exitflag,
+                           int32_t* inner_iters, int nthreads) {
+    return ntm_oracle_step_gen(p, c, NULL, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters,
+                               nthreads);
+}
+
+/* Batched closed loop NTM_MPC_Sim.m:80-131.  Output layouts as ntm_mpc_run;
+ * gen may be NULL, plant step kk uses time index gen->k0 + kk. */
+EXPORT int ntm_oracle_run_gen(const ntm_physics* p, const ntm_config* c, const ntm_scenario_gen* gen,
+                              int64_t B, int32_t k_sim, const double* x0, double* xk, double* uk, double* Uk,
+                              double* wpred, int32_t* exitflag, int32_t* inner_iters, int nthreads) {
     if (!valid(c) || B < 0 || k_sim < 0) return NTM_E_INVALID;
-    orc_coef k; orc_coeffs(p, c, &k);
+    orc_coef k0; orc_coeffs(p, c, &k0);
     int N = c->N;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #pragma omp parallel for schedule(dynamic, 4)
 #endif
     for (int64_t s = 0; s < B; ++s) {
-        double x[2], rh[3 * NMAX], uo[NMAX], u[NMAX], xp[2 * (NMAX + 1)], xn[2];
+        double x[2], rh[3 * NMAX], uo[NMAX], u[NMAX], xp[2 * (NMAX + 1)], xn[2], d[2];
+        orc_coef k; orc_scn_coeffs(p, c, gen, s, &k0, &k);
         x[0] = x0[s]; x[1] = x0[B + s];
         orc_rho(&k, x, rh);
         for (int i = 1; i < N; ++i) for (int e = 0; e < 3; ++e) rh[3 * i + e] = rh[e];
@@ -751,7 +833,8 @@ EXPORT int ntm_oracle_run(const ntm_physics* p, const ntm_config* c, int64_t B, 
         if (xk) { xk[s] = x[0]; xk[B + s] = x[1]; }
         for (int kk = 0; kk < k_sim; ++kk) {
             int fl, its;
-            orc_step(&k, c, x, rh, uo, u, xp, xn, &fl, &its);
+            if (gen) orc_disturbance(gen, gen->first_id + s, gen->k0 + kk, d);
+            orc_step(&k, c, x, rh, uo, u, xp, xn, &fl, &its, gen ? d : NULL);
             if (uk) uk[(int64_t)kk * B + s] = u[0];
             if (Uk) for (int j = 0; j < N; ++j) Uk[((int64_t)kk * N + j) * B + s] = u[j];
             if (wpred) for (int i = 0; i <= N; ++i) wpred[((int64_t)kk * (N + 1) + i) * B + s] = xp[2 * i];
@@ -762,4 +845,21 @@ EXPORT int ntm_oracle_run(const ntm_physics* p, const ntm_config* c, int64_t B, 
         }
     }
     return 0;
+}
+
+EXPORT int ntm_oracle_run(const ntm_physics* p, const ntm_config* c, int64_t B, int32_t k_sim,
+                          const double* x0, double* xk, double* uk, double* Uk, double* wpred,
+                          int32_t* exitflag, int32_t* inner_iters, int nthreads) {
+    return ntm_oracle_run_gen(p, c, NULL, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, nthreads);
+}
+
+/* The generator's samples (same layout as the library's ntm_scenario_sample). */
+EXPORT void ntm_oracle_scenario_sample(const ntm_scenario_gen* g, int64_t B, int32_t k, double* out4) {
+    for (int64_t s = 0; s < B; ++s) {
+        int64_t id = g->first_id + s;
+        out4[4 * s] = o_factor(g->seed, id, 0, g->jbs_spread);
+        out4[4 * s + 1] = o_factor(g->seed, id, 1, g->wdep_spread);
+        out4[4 * s + 2] = o_normal(g->seed, id, (uint32_t)k, 0);
+        out4[4 * s + 3] = o_normal(g->seed, id, (uint32_t)k, 1);
+    }
 }

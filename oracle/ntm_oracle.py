@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+from fractions import Fraction
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -699,7 +700,7 @@ def initial_rho(x0, phys: Physics, cfg: Config):
     return np.tile(rho_all(np.asarray(x0, dtype=float), phys, cfg)[:, None], (1, cfg.N))
 
 
-def mpc_step(xk, Rho, Uold, phys: Physics, cfg: Config, polish=False):
+def mpc_step(xk, Rho, Uold, phys: Physics, cfg: Config, polish=False, dist=None):
     """One MPC time step for one scenario: NTM_MPC_Sim.m:94-130 (CANON ordering
     per SURVEY.md §2.1: build -> QP -> rollout -> rho update -> convergence).
 
@@ -723,15 +724,23 @@ def mpc_step(xk, Rho, Uold, phys: Physics, cfg: Config, polish=False):
             break                                            # :125, before :127
         Uold = U.copy()                                      # :127 (skipped on break)
     xn = plant_step(xk, U[0], phys, cfg)
+    if dist is not None:                                     # scenario generator (plant only)
+        xn = np.array([xn[0] + dist[0] if dist[0] != 0.0 else xn[0],
+                       xn[1] + dist[1] if dist[1] != 0.0 else xn[1]])
     return {"U": U, "u": U[0], "xpred": xp, "xnext": xn, "Rho": Rho, "Uold": Uold,
             "exitflag": flag, "inner_iters": it}
 
 
-def closed_loop(x0, phys: Physics, cfg: Config, k_sim=20, polish=False):
+def closed_loop(x0, phys: Physics, cfg: Config, k_sim=20, polish=False, gen=None, sid=0):
     """NTM_MPC_Sim.m:80-131 for one scenario.  Returns the workspace
     variables xk (2 x k_sim+1), uk (k_sim), Uk (N x k_sim) plus per-step
-    exitflag / inner iteration counts and the last predicted trajectories."""
+    exitflag / inner iteration counts and the last predicted trajectories.
+    ``gen`` (ScenarioGen) makes it global scenario ``gen.first_id + sid``:
+    its own plasma (scenario_physics) and plant disturbances at time indices
+    gen.k0 + k."""
     N = cfg.N
+    if gen is not None:
+        phys = scenario_physics(phys, gen, gen.first_id + sid)
     xk = np.zeros((2, k_sim + 1))
     xk[:, 0] = x0
     uk = np.zeros(k_sim)
@@ -742,7 +751,8 @@ def closed_loop(x0, phys: Physics, cfg: Config, k_sim=20, polish=False):
     Rho = initial_rho(x0, phys, cfg)
     Uold = np.full(N, np.inf)                                 # D14
     for k in range(k_sim):
-        out = mpc_step(xk[:, k], Rho, Uold, phys, cfg, polish=polish)
+        d = None if gen is None else disturbance(gen, gen.first_id + sid, gen.k0 + k)
+        out = mpc_step(xk[:, k], Rho, Uold, phys, cfg, polish=polish, dist=d)
         Rho, Uold = out["Rho"], out["Uold"]
         Uk[:, k] = out["U"]
         uk[k] = out["u"]
@@ -781,3 +791,61 @@ def scenario_x0(ids, seed=20241220):
         out[k, 0] = 0.07 + 0.07 * u0
         out[k, 1] = (0.8 + 0.4 * u1) * 2000 * math.pi
     return out
+
+
+# --------------------------------------------------------------------------
+# Scenario generator (include/ntm_mpc.h ntm_scenario_gen): independent plasma
+# scenarios (j_BS, w_dep of NTM_MPC_Sim.m:5-6) and plant disturbance
+# realisations (added to the plant step NTM_MPC_Sim.m:130), counter-based on
+# (seed, global scenario id, time index)
+# --------------------------------------------------------------------------
+_M64 = 0xFFFFFFFFFFFFFFFF
+GEN_PARAM_K = 0xFFFFFFFF
+
+
+@dataclass
+class ScenarioGen:
+    seed: int = 20241220
+    first_id: int = 0
+    k0: int = 0
+    sigma_w: float = 0.0          # [m] per plant step
+    sigma_omega: float = 0.0      # [rad/s] per plant step
+    jbs_spread: float = 0.0       # j_BS (1 + spread (2u - 1))
+    wdep_spread: float = 0.0      # w_dep (1 + spread (2u - 1))
+
+
+def gen_u01(seed, sid, k, ch):
+    """Uniform [0, 1): splitmix64 chain over (seed, id, k, ch)."""
+    h = _splitmix64((seed ^ 0xD1B54A32D192ED03) & _M64)
+    h = _splitmix64(h ^ (sid & _M64))
+    h = _splitmix64(h ^ ((((k & 0xFFFFFFFF) << 8) | ch) & _M64))
+    return (h >> 11) * (1.0 / 9007199254740992.0)
+
+
+def gen_normal(seed, sid, k, c):
+    """Irwin-Hall(4) unit-variance sample, channel c (sub-channels 4c..4c+3)."""
+    s = gen_u01(seed, sid, k, 4 * c)
+    s = s + gen_u01(seed, sid, k, 4 * c + 1)
+    s = s + gen_u01(seed, sid, k, 4 * c + 2)
+    s = s + gen_u01(seed, sid, k, 4 * c + 3)
+    return (s - 2.0) * 1.7320508075688772
+
+
+def gen_factor(seed, sid, c, spread):
+    """1 + spread (2u - 1) with ONE rounding (a fused multiply-add, as the C-ABI and the
+    device compute it): exact rational arithmetic, then one correctly rounded float()."""
+    t = 2.0 * gen_u01(seed, sid, GEN_PARAM_K, c) - 1.0          # exact
+    return float(Fraction(spread) * Fraction(t) + 1)
+
+
+def scenario_physics(phys: Physics, gen: ScenarioGen, sid: int) -> Physics:
+    """Global scenario sid's plasma: j_BS and w_dep scaled by their factors."""
+    return dataclasses.replace(phys, j_BS=phys.j_BS * gen_factor(gen.seed, sid, 0, gen.jbs_spread),
+                               w_dep=phys.w_dep * gen_factor(gen.seed, sid, 1, gen.wdep_spread))
+
+
+def disturbance(gen: ScenarioGen, sid: int, k: int):
+    """Additive plant disturbance [d_w, d_omega] of scenario sid at time index k."""
+    dw = gen.sigma_w * gen_normal(gen.seed, sid, k, 0) if gen.sigma_w != 0.0 else 0.0
+    do = gen.sigma_omega * gen_normal(gen.seed, sid, k, 1) if gen.sigma_omega != 0.0 else 0.0
+    return np.array([dw, do])

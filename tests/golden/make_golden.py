@@ -36,15 +36,36 @@ def functions_fixture(N):
              W=W, L=L, c=c, A0=A0, B0=B0, C=O.C_vec(ph, cfg.Ts), kappa=ph.kappa(), zeta=ph.zeta())
 
 
-def closed_loop_fixture(N, mode, ids, k_sim):
+def closed_loop_fixture(N, mode, ids, k_sim, gen=None, name=None):
+    """Closed loops (NTM_MPC_Sim.m:80-131).  wpred (k_sim, N+1) is the predicted
+    island width of every step's last rollout (:110-117); with ``gen`` the
+    scenarios are global ids gen.first_id + s of the scenario generator."""
     ph = O.Physics()
     cfg = O.Config(N=N, mode=mode)
     x0 = O.scenario_x0(ids) if mode != O.MODE_NONE else np.tile(O.REFERENCE_X0, (len(ids), 1))
-    outs = [O.closed_loop(x0[s], ph, cfg, k_sim) for s in range(len(ids))]
-    np.savez(HERE / f"closed_loop_m{mode}_N{N}.npz", x0=x0, ids=np.asarray(ids),
+    outs = [O.closed_loop(x0[s], ph, cfg, k_sim, gen=gen, sid=s) for s in range(len(ids))]
+    extra = {}
+    if gen is not None:
+        extra = dict(gen_seed=gen.seed, gen_first_id=gen.first_id, gen_k0=gen.k0, gen_sigma_w=gen.sigma_w,
+                     gen_sigma_omega=gen.sigma_omega, gen_jbs_spread=gen.jbs_spread,
+                     gen_wdep_spread=gen.wdep_spread)
+    np.savez(HERE / (name or f"closed_loop_m{mode}_N{N}.npz"), x0=x0, ids=np.asarray(ids),
              xk=np.stack([o["xk"] for o in outs]), uk=np.stack([o["uk"] for o in outs]),
-             Uk=np.stack([o["Uk"] for o in outs]), exitflag=np.stack([o["exitflag"] for o in outs]),
-             inner_iters=np.stack([o["inner_iters"] for o in outs]), k_sim=k_sim)
+             Uk=np.stack([o["Uk"] for o in outs]), wpred=np.stack([o["xpred"][:, 0, :] for o in outs]),
+             exitflag=np.stack([o["exitflag"] for o in outs]),
+             inner_iters=np.stack([o["inner_iters"] for o in outs]), k_sim=k_sim, **extra)
+
+
+def literal_functions_fixture(N, flags):
+    """Rho_to_PhiGammaLambda.m with the literal-reference switches D4
+    (Phi_{j-1} A_j, :21) and D6 (A(rho_{i-j}), :32)."""
+    ph = O.Physics()
+    cfg = O.Config(N=N, mode=O.MODE_FULL, flags=flags)
+    rng = np.random.default_rng(2000 + N + flags)
+    xs = np.stack([rng.uniform(0.06, 0.15, N), rng.uniform(0.8, 1.2, N) * 2000 * np.pi])
+    Rho = np.stack([O.rho_all(xs[:, i], ph, cfg) for i in range(N)], axis=1)
+    Phi, Gam, Lam = O.lift(Rho, ph, cfg)
+    np.savez(HERE / f"functions_lit{flags}_N{N}.npz", Rho=Rho, Phi=Phi, Gamma=Gam, Lambda=Lam, flags=flags)
 
 
 def qp_fixture(N, mode, n):
@@ -73,20 +94,38 @@ def qp_fixture(N, mode, n):
              U_exact=np.stack(Us), exitflag=np.asarray(flags))
 
 
-def main():
-    for N in (3, 20):
-        functions_fixture(N)
-    closed_loop_fixture(10, O.MODE_NONE, [0], 20)          # BASELINE config 1
-    closed_loop_fixture(3, O.MODE_FULL, [0, 1, 2, 3], 20)
-    closed_loop_fixture(20, O.MODE_BOX, [0, 1], 6)          # config 2 shape
-    closed_loop_fixture(20, O.MODE_FULL, [0, 1, 2], 6)      # config 3 shape
-    qp_fixture(20, O.MODE_FULL, 12)
-    qp_fixture(20, O.MODE_BOX, 8)
-    # BASELINE config 5 row structure (input-rate rows, an extension of getWLc)
-    closed_loop_fixture(20, O.MODE_FULL_DU, [0, 1], 6)
-    qp_fixture(20, O.MODE_FULL_DU, 8)
+GEN = O.ScenarioGen(seed=20241220, first_id=0, k0=0, sigma_w=1e-3, sigma_omega=0.0, jbs_spread=0.1,
+                    wdep_spread=0.1)
+
+
+def main(which=("functions", "closed_loop", "qp", "literal", "gen")):
+    if "literal" in which:
+        for flags in (O.LITERAL_PHI_RIGHTMUL, O.LITERAL_GAMMA_INDEX,
+                      O.LITERAL_PHI_RIGHTMUL | O.LITERAL_GAMMA_INDEX):
+            literal_functions_fixture(6, flags)
+    if "gen" in which:
+        # disturbance realisations + plasma scenarios (SURVEY.md §8d sigma_w = 1e-3 m)
+        closed_loop_fixture(20, O.MODE_FULL, [0, 1, 2], 8, gen=GEN, name="closed_loop_gen_m2_N20.npz")
+        closed_loop_fixture(3, O.MODE_FULL, [0, 1, 2, 3], 20, gen=GEN, name="closed_loop_gen_m2_N3.npz")
+    if "functions" in which:
+        for N in (3, 20):
+            functions_fixture(N)
+    if "closed_loop" not in which and "qp" not in which:
+        print("fixtures written to", HERE)
+        return
+    if "closed_loop" in which:
+        closed_loop_fixture(10, O.MODE_NONE, [0], 20)          # BASELINE config 1
+        closed_loop_fixture(3, O.MODE_FULL, [0, 1, 2, 3], 20)
+        closed_loop_fixture(20, O.MODE_BOX, [0, 1], 6)          # config 2 shape
+        closed_loop_fixture(20, O.MODE_FULL, [0, 1, 2], 6)      # config 3 shape
+        # BASELINE config 5 row structure (input-rate rows, an extension of getWLc)
+        closed_loop_fixture(20, O.MODE_FULL_DU, [0, 1], 6)
+    if "qp" in which:
+        qp_fixture(20, O.MODE_FULL, 12)
+        qp_fixture(20, O.MODE_BOX, 8)
+        qp_fixture(20, O.MODE_FULL_DU, 8)
     print("fixtures written to", HERE)
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]) or ("functions", "closed_loop", "qp", "literal", "gen"))

@@ -202,7 +202,7 @@ def test_step_teacher_forced_weighted(ctl, N, mode, warm):
     _teacher_forced(ctl, N, mode, warm, k_sim=6, Q=(2.0e4, 3.0, 3.0, 2.0e-2), r=(0.09, 900 * 2 * math.pi))
 
 
-def _teacher_forced(ctl, N, mode, warm, k_sim=None, **kw):
+def _teacher_forced(ctl, N, mode, warm, k_sim=None, gen=None, **kw):
     """Each step, the GPU and the oracle get identical (x_k, rho, U_old); with
     warm=True the GPU also carries its active-set workspace from step to step
     (ntm_mpc_step_ws_device), which must not change the answer.
@@ -215,17 +215,35 @@ def _teacher_forced(ctl, N, mode, warm, k_sim=None, **kw):
     DESIGN.md §3) legitimately ends elsewhere: there the scenarios that took
     the same path are compared directly (>= 90% of them must have), and the
     others against the oracle re-run along the GPU's path (the GPU's
-    inner-iteration count, no early stop), to the same tolerance."""
+    inner-iteration count, no early stop), to the same tolerance.
+
+    ``gen`` (oracle ScenarioGen): each scenario runs its own plasma and step k's
+    plant step adds its disturbance at time index k, on both sides."""
     B, ks = (48, 12) if N < 50 else ((48, 4) if N == 50 else (16, 3))
     k_sim = min(ks, k_sim) if k_sim else ks
     cfg, ocfg = cfgs(N, mode, **kw)
     x = O.scenario_x0(np.arange(B)).T if mode else np.tile(O.REFERENCE_X0[:, None], (1, B))
-    rho, Uo = cbind.initial_state(x, ocfg)
+    if gen is None:
+        rho, Uo = cbind.initial_state(x, ocfg)
+    else:
+        rho, Uo = cbind.initial_state_gen(x, ocfg, gen)
+    try:
+        _teacher_forced_loop(ctl, N, mode, warm, k_sim, gen, cfg, ocfg, B, x, rho, Uo)
+    finally:
+        if gen is not None:
+            ctl.set_scenarios(None)
+
+
+def _teacher_forced_loop(ctl, N, mode, warm, k_sim, gen, cfg, ocfg, B, x, rho, Uo):
+    from ntm_mpc import ScenarioGen
     ws = ctl.new_active_ws(B, cfg) if warm else None
     worst, worst_div, same_iters, n = 0.0, 0.0, 0, 0
     xscale = np.array([0.15, 2000 * math.pi])[:, None]      # |w|, |omega| magnitudes
     for k in range(k_sim):
-        ref = cbind.step(x, rho, Uo, ocfg)
+        ogen = None if gen is None else dataclasses.replace(gen, k0=k)
+        if gen is not None:
+            ctl.set_scenarios(ScenarioGen(**dataclasses.asdict(ogen)))
+        ref = cbind.step(x, rho, Uo, ocfg, gen=ogen)
         tr, tu = T(rho), T(Uo)
         out = ctl.step(T(x), tr, tu, cfg, active_ws=ws)
         assert (H(out["exitflag"]) == ref["exitflag"]).all(), k
@@ -397,15 +415,29 @@ def test_step_ragged_batches(ctl, B):
 # ---------------------------------------------------------------- closed loop
 @pytest.mark.parametrize("N,mode", [(10, 0), (20, 1), (20, 2), (20, 3)])
 def test_run_closed_loop(ctl, N, mode):
+    """ntm_mpc_run (NTM_MPC_Sim.m:80-131) against the C oracle's closed loop: every
+    workspace output north_star names, the applied inputs uk, the plans Uk
+    (:106), the states xk and the predicted island width wpred (x_pred's w row,
+    :110-117), free-running (rounding amplified by the loop: 1e-6)."""
     B, k_sim = 32, 20
     cfg, ocfg = cfgs(N, mode)
     x0 = O.scenario_x0(np.arange(B)).T if mode else np.tile(O.REFERENCE_X0[:, None], (1, B))
     ref = cbind.run(x0, ocfg, k_sim)
     out = ctl.run(T(x0), k_sim, cfg)
+    _assert_run_close(out, ref, cfg, k_sim)
+
+
+def _assert_run_close(out, ref, cfg, k_sim, tol=1e-6):
+    N = cfg.N
     du = np.max(np.abs(H(out["uk"]) - ref["uk"])) / cfg.umax
-    assert du <= 1e-6, du
+    assert du <= tol, du
+    dU = np.max(np.abs(H(out["Uk"]) - ref["Uk"])) / cfg.umax
+    assert dU <= tol, dU
     xscale = np.tile(np.array([0.15, 2000 * math.pi]), k_sim + 1)[:, None]
-    assert np.max(np.abs(H(out["xk"]) - ref["xk"]) / xscale) <= 1e-6
+    assert np.max(np.abs(H(out["xk"]) - ref["xk"]) / xscale) <= tol
+    dw = np.max(np.abs(H(out["wpred"]) - ref["wpred"])) / 0.15
+    assert dw <= tol, dw
+    assert H(out["wpred"]).shape == ((N + 1) * k_sim, ref["wpred"].shape[1])
     assert (H(out["exitflag"]) == ref["exitflag"]).mean() > 0.99
 
 

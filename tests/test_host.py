@@ -80,6 +80,45 @@ def test_scenario_generator_matches_oracle():
     np.testing.assert_array_equal(a[:, 5:], b)
 
 
+def test_disturbance_generator_matches_both_oracles():
+    """ntm_scenario_sample (the device's generator code compiled for the host) ==
+    the C oracle == the NumPy oracle, bit for bit, for plasma factors and
+    disturbance samples; counter-based (a shard's first_id offset reproduces the
+    same values); the samples have zero mean and unit variance and the factors
+    stay inside 1 +- spread."""
+    import ntm_mpc
+    from oracle import cbind
+    from oracle import ntm_oracle as O
+    for seed, first, k in ((20241220, 0, 0), (7, -5, 13), (2 ** 64 - 1, 10 ** 12, 2 ** 31 - 1)):
+        g = O.ScenarioGen(seed=seed, first_id=first, k0=0, sigma_w=1e-3, sigma_omega=1.0, jbs_spread=0.1,
+                          wdep_spread=0.37)
+        lib = ntm_mpc.scenario_sample(ntm_mpc.ScenarioGen(**vars(g)), 300, k)
+        np.testing.assert_array_equal(lib, cbind.scenario_sample(g, 300, k))
+        py = np.array([[O.gen_factor(seed, first + s, 0, 0.1), O.gen_factor(seed, first + s, 1, 0.37),
+                        O.gen_normal(seed, first + s, k, 0), O.gen_normal(seed, first + s, k, 1)]
+                       for s in range(300)])
+        np.testing.assert_array_equal(lib, py)
+        shard = ntm_mpc.scenario_sample(ntm_mpc.ScenarioGen(**{**vars(g), "first_id": first + 100}), 200, k)
+        np.testing.assert_array_equal(shard, lib[100:])
+    big = ntm_mpc.scenario_sample(ntm_mpc.ScenarioGen(seed=3, jbs_spread=0.1, wdep_spread=0.1), 200_000, 5)
+    n = big[:, 2:].ravel()
+    assert abs(n.mean()) < 0.01 and abs(n.std() - 1.0) < 0.01
+    assert np.abs(n).max() <= 2 * math.sqrt(3)
+    assert big[:, :2].min() >= 0.9 and big[:, :2].max() < 1.1
+    assert abs(np.corrcoef(big[:, 2], big[:, 3])[0, 1]) < 0.01
+    # different time indices give independent draws
+    other = ntm_mpc.scenario_sample(ntm_mpc.ScenarioGen(seed=3), 200_000, 6)
+    assert abs(np.corrcoef(big[:, 2], other[:, 2])[0, 1]) < 0.01
+
+
+def test_scenario_gen_struct_layout():
+    """ctypes mirrors of ntm_scenario_gen agree with the C layout (56 bytes)."""
+    from ntm_mpc._lib import NtmScenarioGen
+    from oracle.cbind import CGen
+    assert C.sizeof(NtmScenarioGen) == C.sizeof(CGen) == 56
+    assert NtmScenarioGen.sigma_w.offset == 24 and NtmScenarioGen.wdep_spread.offset == 48
+
+
 def test_no_gpu_raises_not_falls_back():
     import torch
     if torch.cuda.is_available():

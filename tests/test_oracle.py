@@ -296,14 +296,26 @@ def test_closed_loop_golden(name):
 def test_lpv_loop_semantics():
     """NTM_MPC_Sim.m:94-127: the LPV loop runs at most i_sim QPs, stops when
     sum|U - Uold| < eps, carries rho unshifted (D20) and Uold across steps (D14),
-    and the applied input is U(1) of the last QP (D21)."""
+    and the applied input is U(1) of the last QP (D21).  Uold follows the
+    reference order: the break at :125 comes before Uold = Uk(:,k) at :127, so
+    on the converging iteration Uold stays the previous iterate (within eps of
+    U, not necessarily bit-equal); only a loop that ran to i_sim ends with
+    Uold == U."""
+    for c in (cfg(3), cfg(3, i_sim=3), cfg(3, epsilon=1.0)):
+        x0 = O.scenario_x0([0])[0]
+        Rho = O.initial_rho(x0, PH, c)
+        st = O.mpc_step(x0, Rho, np.full(3, np.inf), PH, c)
+        assert 1 <= st["inner_iters"] <= c.i_sim
+        assert st["u"] == st["U"][0]
+        d = float(np.sum(np.abs(st["Uold"] - st["U"])))
+        if st["inner_iters"] < c.i_sim:
+            assert d < c.epsilon
+        else:
+            assert d < c.epsilon or np.array_equal(st["Uold"], st["U"])
     c = cfg(3)
     x0 = O.scenario_x0([0])[0]
     Rho = O.initial_rho(x0, PH, c)
     st = O.mpc_step(x0, Rho, np.full(3, np.inf), PH, c)
-    assert 1 <= st["inner_iters"] <= c.i_sim
-    assert st["u"] == st["U"][0]
-    np.testing.assert_array_equal(st["Uold"], st["U"])
     xp, Rn = O.rollout(x0, Rho, st["U"], PH, c)        # rho_i <- rho(x_{i-1})
     np.testing.assert_allclose(Rn[:, 0], O.rho_all(x0, PH, c))
     c1 = cfg(3, i_sim=1)
