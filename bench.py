@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--sigma-w", type=float, default=1e-3, help="disturbed leg: w disturbance per step [m]")
     ap.add_argument("--spread", type=float, default=0.1, help="disturbed leg: j_BS / w_dep spread over scenarios")
     ap.add_argument("--verify", type=int, default=64, help="scenarios rank 0 recomputes after the gather")
+    ap.add_argument("--no-stats", action="store_true",
+                    help="A/B only: leave the solver counters off in the timed region (roofline then unavailable)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample length")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse the multi-rank "
@@ -151,7 +153,7 @@ def _workload(N, mode, B):
     return f"{tag}: LPV-MPC closed-loop step, N={N}, {kind}, B={B} per GPU, fp64"
 
 
-def _run_leg(ctl, cfg, B, K, W, x0, rank, world, gen=None, collect=False):
+def _run_leg(ctl, cfg, B, K, W, x0, rank, world, gen=None, collect=False, stats_on=True):
     """W untimed warmup steps then K timed steps of the closed loop through the
     step entry point, the solver counters accumulated over exactly the K timed
     launches.  Returns timing, per-step counters and (collect) the histories."""
@@ -186,7 +188,7 @@ def _run_leg(ctl, cfg, B, K, W, x0, rank, world, gen=None, collect=False):
                 "inner_iters": torch.empty(K, B, dtype=torch.int32, device=dev)}
         hist["xk"][0].copy_(x)
     stats = torch.zeros(STATS_ROWS, B, dtype=torch.int32, device=dev)
-    ctl.set_stats(stats)
+    ctl.set_stats(stats if stats_on else None)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     if world > 1:
         dist.barrier()
@@ -270,7 +272,7 @@ def main():
     # shard: global scenario ids [rank*B, (rank+1)*B)  (shard-invariant inputs)
     x0 = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(rank * B, B), local)
 
-    leg = _run_leg(ctl, cfg, B, K, W, x0, rank, world, collect=True)
+    leg = _run_leg(ctl, cfg, B, K, W, x0, rank, world, collect=True, stats_on=not args.no_stats)
     # end-of-batch gather of every per-scenario output history (RCCL over xGMI;
     # gloo rehearsal through host memory), scenario order = global id order
     g = None

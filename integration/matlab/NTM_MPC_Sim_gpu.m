@@ -1,4 +1,4 @@
-function [xk, uk, Uk, exitflag, iters] = NTM_MPC_Sim_gpu(x0, k_sim, cfg, mode)
+function [xk, uk, Uk, exitflag, iters, wpred] = NTM_MPC_Sim_gpu(x0, k_sim, cfg, mode, gen)
 %NTM_MPC_SIM_GPU  Drop-in for the controller loop of NTM_MPC_Sim.m (lines 80-131)
 %   on MI355X, for one or many scenarios at once.
 %
@@ -11,6 +11,10 @@ function [xk, uk, Uk, exitflag, iters] = NTM_MPC_Sim_gpu(x0, k_sim, cfg, mode)
 %           literals (NTM_MPC_Sim.m:30-88)
 %     mode  'run' (default): the whole closed loop on the device, one call;
 %           'step': one MEX call per time step (the state stays in MATLAB)
+%     gen   optional scenario generator struct (seed, first_id, sigma_w,
+%           sigma_omega, jbs_spread, wdep_spread): independent plasma
+%           scenarios and plant disturbance realisations (ntm_scenario_gen);
+%           omitted = the reference's nominal, disturbance-free loop
 %   Returns the reference's workspace variables with a trailing scenario
 %   dimension: xk 2-by-(k_sim+1)-by-B, uk 1-by-k_sim-by-B, Uk N-by-k_sim-by-B,
 %   plus exitflag / iters (k_sim-by-B, quadprog codes and LPV iterations).
@@ -23,26 +27,34 @@ function [xk, uk, Uk, exitflag, iters] = NTM_MPC_Sim_gpu(x0, k_sim, cfg, mode)
 %   from the current x_k, plant step with +C, Uold = +Inf at start.
 if nargin < 3, cfg = struct(); end
 if nargin < 4, mode = 'run'; end
+if nargin < 5, gen = []; end
+if isempty(gen), ntm_mpc_mex('scenarios', []); else, ntm_mpc_mex('scenarios', gen); end
 if ~isfield(cfg, 'N'), cfg.N = 20; end
 N = cfg.N;
 B = size(x0, 2);
 switch mode
     case 'run'
-        [XK, UK, UKK, ~, FL, IT] = ntm_mpc_mex('run', x0, k_sim, cfg);
+        [XK, UK, UKK, WP, FL, IT] = ntm_mpc_mex('run', x0, k_sim, cfg);
         xk = reshape(XK, 2, k_sim + 1, B);
         uk = reshape(UK, 1, k_sim, B);
         Uk = reshape(UKK, N, k_sim, B);
+        wpred = reshape(WP, N + 1, k_sim, B);   % predicted island width per step (:110-117)
         exitflag = FL;
         iters = IT;
     case 'step'
         xk = zeros(2, k_sim + 1, B); uk = zeros(1, k_sim, B); Uk = zeros(N, k_sim, B);
+        wpred = zeros(N + 1, k_sim, B);
         exitflag = zeros(k_sim, B, 'int32'); iters = zeros(k_sim, B, 'int32');
         xk(:, 1, :) = reshape(x0, 2, 1, B);
         [Rho, Uold] = ntm_mpc_mex('init', x0, cfg);   % Rho = repmat(rho(x0),1,N), Uold = +Inf
         WS = -ones(2 * (N + 1), B, 'int32');         % warm-start workspace, carried step to step
         X = x0;
         for k = 1:k_sim
-            [U, ~, Xn, fl, it, Rho, Uold, WS] = ntm_mpc_mex('step', X, Rho, Uold, cfg, WS);
+            if ~isempty(gen)                         % the plant step's time index
+                gen.k0 = k - 1; ntm_mpc_mex('scenarios', gen);
+            end
+            [U, XP, Xn, fl, it, Rho, Uold, WS] = ntm_mpc_mex('step', X, Rho, Uold, cfg, WS);
+            wpred(:, k, :) = reshape(XP(1:2:end, :), N + 1, 1, B);
             Uk(:, k, :) = reshape(U, N, 1, B);
             uk(1, k, :) = reshape(U(1, :), 1, 1, B);
             exitflag(k, :) = fl; iters(k, :) = it;

@@ -25,6 +25,11 @@
  *   [xk, uk, Uk, wpred, exitflag, iters] = ntm_mpc_mex('run', x0, k_sim, cfg)
  *       outputs 2(k_sim+1)-by-B, k_sim-by-B, N k_sim-by-B, (N+1) k_sim-by-B,
  *       k_sim-by-B, k_sim-by-B (per scenario column: xk(:), uk, Uk(:), ...)
+ *   ntm_mpc_mex('scenarios', gen)                               
+ *       gen struct with any of seed, first_id, k0, sigma_w, sigma_omega,
+ *       jbs_spread, wdep_spread (ntm_scenario_gen): per-scenario plasma and
+ *       plant disturbances for the following init/step/run calls; [] = off.
+ *       With 'step', set k0 to the step's time index before each call.
  *   ntm_mpc_mex('close')
  *
  * cfg is an optional struct with any of the fields N, i_sim, mode, flags, Ts,
@@ -180,14 +185,34 @@ static void do_run(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     }
 }
 
+static void do_scenarios(int nrhs, const mxArray* prhs[]) {
+    if (nrhs < 2 || (mxIsDouble(prhs[1]) && mxGetNumberOfElements(prhs[1]) == 0)) {
+        check(ntm_ctx_set_scenarios(ctx(), NULL), "ntm_ctx_set_scenarios");
+        return;
+    }
+    const mxArray* s = prhs[1];
+    if (!mxIsStruct(s)) mexErrMsgIdAndTxt("ntm:arg", "gen must be a struct or []");
+    ntm_scenario_gen g;
+    memset(&g, 0, sizeof g);
+    g.seed = (uint64_t)scalar_field(s, "seed", 20241220);
+    g.first_id = (int64_t)scalar_field(s, "first_id", 0);
+    g.k0 = (int32_t)scalar_field(s, "k0", 0);
+    g.sigma_w = scalar_field(s, "sigma_w", 0.0);
+    g.sigma_omega = scalar_field(s, "sigma_omega", 0.0);
+    g.jbs_spread = scalar_field(s, "jbs_spread", 0.0);
+    g.wdep_spread = scalar_field(s, "wdep_spread", 0.0);
+    check(ntm_ctx_set_scenarios(ctx(), &g), "ntm_ctx_set_scenarios");
+}
+
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     if (nrhs < 1 || !mxIsChar(prhs[0]))
-        mexErrMsgIdAndTxt("ntm:arg", "first argument: 'init', 'step', 'run' or 'close'");
+        mexErrMsgIdAndTxt("ntm:arg", "first argument: 'init', 'step', 'run', 'scenarios' or 'close'");
     char cmd[16];
     mxGetString(prhs[0], cmd, sizeof cmd);
     if (!strcmp(cmd, "step")) do_step(nlhs, plhs, nrhs, prhs);
     else if (!strcmp(cmd, "init")) do_init(nlhs, plhs, nrhs, prhs);
     else if (!strcmp(cmd, "run")) do_run(nlhs, plhs, nrhs, prhs);
+    else if (!strcmp(cmd, "scenarios")) do_scenarios(nrhs, prhs);
     else if (!strcmp(cmd, "close")) release();
     else mexErrMsgIdAndTxt("ntm:arg", "unknown command '%s'", cmd);
 }

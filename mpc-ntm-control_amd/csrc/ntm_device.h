@@ -373,9 +373,13 @@ __device__ __forceinline__ double coef_b(const Coef& k, double r3) { return k.bc
 // ---------------------------------------------------------------------------
 // NN > 0: horizon fixed at compile time (strides become immediates, loops
 // unroll); NN == 0: runtime horizon (generic kernels).
-template <int NN>
+// GEN: the kernel is built with the scenario generator (per-scenario plasma in
+// the workspace, plant disturbances); without it those paths are compiled out
+// (they cost the N=20 step kernel 2% through register allocation even when off)
+template <int NN, bool GEN = false>
 struct WS {
     static constexpr int kNN = NN;
+    static constexpr bool kGen = GEN;
     int N_rt;
     double* base;
     __device__ __forceinline__ int n() const { return NN > 0 ? NN : N_rt; }
@@ -458,9 +462,9 @@ __host__ __device__ inline int ws_bytes_rows(int N, int rows) {
 }
 __host__ __device__ inline int ws_bytes(int N) { return ws_bytes_rows(N, 8 * N + 4); }
 
-template <int NN>
-__device__ inline WS<NN> ws_carve(char* base, int N) {
-    WS<NN> w;
+template <int NN, bool GEN = false>
+__device__ inline WS<NN, GEN> ws_carve(char* base, int N) {
+    WS<NN, GEN> w;
     w.N_rt = N;
     w.base = reinterpret_cast<double*>(base);
     return w;
@@ -471,10 +475,12 @@ __device__ inline WS<NN> ws_carve(char* base, int N) {
 // (written once per launch by scn_store).  Keeping the launch constants in the
 // kernel arguments matters: a copy of the whole Prob per scenario cost the N=20
 // step kernel 100 B of scratch per lane and 20 more spilled SGPRs.
+__device__ __forceinline__ bool gen_phys(const Prob& pb) { return pb.g.phys_on != 0; }
+__device__ __forceinline__ bool gen_dist(const Prob& pb) { return pb.g.dist_on != 0; }
 template <class W>
 __device__ __forceinline__ Coef scn_coef(const Prob& pb, const W& w) {
     Coef k = pb.k;
-    if (pb.g.phys_on) {
+    if (W::kGen && gen_phys(pb)) {
         k.C1 = w.scn()[0];
         k.bc = w.scn()[1];
         k.wdep = w.scn()[2];
@@ -483,7 +489,7 @@ __device__ __forceinline__ Coef scn_coef(const Prob& pb, const W& w) {
 }
 template <class W>
 __device__ __forceinline__ void scn_store(const Prob& pb, const W& w, int64_t gid, int l) {
-    if (pb.g.phys_on && l == 0) {
+    if (W::kGen && gen_phys(pb) && l == 0) {
         Prob q = pb;
         gen_apply_physics(q, gid);
         w.scn()[0] = q.k.C1;
@@ -2690,6 +2696,7 @@ __device__ __forceinline__ bool rollout_phase(const Prob& pb, const W& w, double
 // plant step NTM_MPC_Sim.m:130 (CANON D13: plant = prediction model, + C), plus
 // the scenario's disturbance realisation at time index kt (ntm_ctx_set_scenarios;
 // the model the controller predicts with does not know it)
+template <bool GEN = false>
 __device__ __forceinline__ void plant_step(const Prob& pb, const Coef& k, double x0, double x1, double u,
                                            double& n0, double& n1, int64_t gid = 0, int kt = 0) {
     double r1, r2, r3;
@@ -2698,7 +2705,7 @@ __device__ __forceinline__ void plant_step(const Prob& pb, const Coef& k, double
     n0 = a11 * x0 + b * u;
     n1 = a21 * x0 + k.a22 * x1;
     if (!(pb.flags & NTM_LITERAL_PLANT_NO_C)) { n0 += k.C1; n1 += k.C2; }
-    if (pb.g.dist_on) {
+    if (GEN && gen_dist(pb)) {
         if (pb.g.sw != 0.0) n0 += pb.g.sw * gen_normal(pb.g.seed, gid, (uint32_t)kt, 0);
         if (pb.g.so != 0.0) n1 += pb.g.so * gen_normal(pb.g.seed, gid, (uint32_t)kt, 1);
     }

@@ -135,7 +135,7 @@ __device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x
 // than SIMDs, so the register budget of one wave per SIMD costs no occupancy and
 // removes the spills of the fully unrolled horizon loops.
 #define NTM_WAVES_PER_EU(NN) ((NN) > 32 ? 1 : NTM_HOT_WAVES_PER_EU)
-template <int P, int NN>
+template <int P, int NN, bool GEN>
 __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, int64_t B, const double* __restrict__ x_k,
                                                  double* __restrict__ rho, double* __restrict__ U_old,
                                                  double* __restrict__ U, double* __restrict__ x_pred,
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, 
     NTM_STAMPS_INIT();
     NTM_TRACE_SET(s, g, l);
     if (s >= B) return;
-    auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
+    auto w = ws_carve<NN, GEN>(smem + g * ws_bytes(N), N);
 #ifdef NTM_POISON
     // debug build (make poison): the workspace starts as NTM_POISON-valued doubles, so
     // a read of LDS this launch never wrote shows up as a run-to-run difference
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, 
     store_record<P>(x_pred + s * (2 * (N + 1)), w.xp(), 2 * (N + 1), l);
     {
         double n0, n1;
-        plant_step(pb, scn_coef(pb, w), x0, x1, w.U()[0], n0, n1, pb.g.first_id + s, pb.g.k0);
+        plant_step<GEN>(pb, scn_coef(pb, w), x0, x1, w.U()[0], n0, n1, pb.g.first_id + s, pb.g.k0);
         if (is16(x_next)) {
             if (l == 0) *reinterpret_cast<double2*>(x_next + 2 * s) = make_double2(n0, n1);
         } else if (l < 2) {
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_run(Prob pb, i
     const int64_t s = xcd_swizzle(blockIdx.x, gridDim.x) * G + g;
     const int N = NN > 0 ? NN : pb.N;
     if (s >= B) return;
-    auto w = ws_carve<NN>(smem + g * ws_bytes(N), N);
+    auto w = ws_carve<NN, true>(smem + g * ws_bytes(N), N);
     double x0 = x0v[2 * s], x1 = x0v[2 * s + 1];
     if (l < 2) w.cand()[l * (N + 1) + N] = -1;
     scn_store(pb, w, pb.g.first_id + s, l);           // this scenario's plasma (generator)
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_run(Prob pb, i
         if (Uk && l < N) Uk[(s * k_sim + kk) * N + l] = w.U()[l];
         if (wpred) for (int i = l; i <= N; i += P) wpred[(s * k_sim + kk) * (N + 1) + i] = w.xp()[2 * i];
         double n0, n1;
-        plant_step(pb, scn_coef(pb, w), x0, x1, w.U()[0], n0, n1, pb.g.first_id + s, pb.g.k0 + kk);
+        plant_step<true>(pb, scn_coef(pb, w), x0, x1, w.U()[0], n0, n1, pb.g.first_id + s, pb.g.k0 + kk);
         if (l == 0) {
             if (uk) uk[s * k_sim + kk] = w.U()[0];
             if (exitflag) exitflag[s * k_sim + kk] = flag;
@@ -590,12 +590,17 @@ int launch_step(ntm_ctx* ctx, const Prob& pb, int64_t B, const double* x_k, doub
 #ifdef NTM_LDS_PAD
     lds += NTM_LDS_PAD;   // occupancy study only (tools/occupancy_study.sh): fewer scenarios per CU
 #endif
-    int rc = set_lds(ctx, k_mpc_step<P, NN>, lds);
+    const bool gen = pb.g.phys_on || pb.g.dist_on;     // the generator's build only when it is used
+    int rc = gen ? set_lds(ctx, k_mpc_step<P, NN, true>, lds) : set_lds(ctx, k_mpc_step<P, NN, false>, lds);
     if (rc) return rc;
     int64_t blocks = (B + G - 1) / G;
     if (blocks == 0) return NTM_OK;
-    hipLaunchKernelGGL((k_mpc_step<P, NN>), dim3((unsigned)blocks), dim3(64), lds, st, pb, B, x_k, rho, U_old, U,
-                       x_pred, x_next, exitflag, inner_iters, active_ws);
+    if (gen)
+        hipLaunchKernelGGL((k_mpc_step<P, NN, true>), dim3((unsigned)blocks), dim3(64), lds, st, pb, B, x_k, rho,
+                           U_old, U, x_pred, x_next, exitflag, inner_iters, active_ws);
+    else
+        hipLaunchKernelGGL((k_mpc_step<P, NN, false>), dim3((unsigned)blocks), dim3(64), lds, st, pb, B, x_k, rho,
+                           U_old, U, x_pred, x_next, exitflag, inner_iters, active_ws);
     return check_hip(ctx, hipGetLastError(), "k_mpc_step launch");
 }
 

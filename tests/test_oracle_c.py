@@ -95,3 +95,21 @@ def test_c_infeasible_and_nonfinite():
     out = cbind.step(x, rho, Uo, c)
     assert out["exitflag"][0] == -2 and np.all(out["U"][:, 0] == 0)
     assert out["exitflag"][1] == -7
+
+
+def test_c_oracle_under_asan_ubsan():
+    """SURVEY.md §5 race/sanitizer row: the C oracle built with AddressSanitizer
+    and UBSan (make -C oracle sanitize), driven through every exported entry
+    point (every mode, N = 1 and 64, all literal switches, the scenario
+    generator, infeasible and non-finite inputs) reports nothing."""
+    import os
+    import subprocess
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    subprocess.run(["make", "-s", "-C", str(root / "oracle"), "sanitize"], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="halt_on_error=1:detect_leaks=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1", OMP_NUM_THREADS="2")
+    r = subprocess.run([str(root / "oracle" / "_san" / "ntm_oracle_san")], capture_output=True, text=True, env=env,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr
