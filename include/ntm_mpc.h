@@ -193,6 +193,18 @@ int ntm_qp_device(ntm_ctx* ctx, int64_t B, int32_t N, int32_t m,
                   const double* b, double* U, int32_t* exitflag,
                   int32_t* iters, void* stream);
 
+/* Mixed precision (BASELINE config 5's "fp32 vs fp64" leg; NOT the fp64 product
+ * path): the same QP as ntm_qp_device solved by Goldfarb-Idnani entirely in
+ * fp32 on fp32-rounded data -> U32[N] (widened), then that active set re-solved
+ * exactly in fp64 with the KKT certificate -> U[N]; if it does not certify, the
+ * fp64 solve takes over.  info: bit 0 the fp32 active set certified, bit 1 fp64
+ * fallback, bit 2 the fp32 solve itself was not optimal.  iters32: fp32 GI
+ * iterations.  N <= 64, m <= 8N+4 rows within the 160 KiB LDS of one CU. */
+int ntm_qp_mixed_device(ntm_ctx* ctx, int64_t B, int32_t N, int32_t m,
+                        const double* G, const double* F, const double* Lin,
+                        const double* b, double* U, double* U32, int32_t* exitflag,
+                        int32_t* info, int32_t* iters32, void* stream);
+
 /* Synthetic scenarios, counter-based and shard-invariant:
  * x0 for global scenario ids first_id .. first_id+B-1 (host array, 2 per scenario). */
 void ntm_scenarios_x0(uint64_t seed, int64_t first_id, int64_t B, double* x0);

@@ -181,7 +181,7 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        ST_S_E, ST_S_Y, ST_S_K, ST_S_CHOL, ST_S_SOLVE, CN_TRY_EARLY, CN_FAIL_EARLY, CN_FAIL_LATE,
        CN_FAIL_IT1, CN_FAIL_IT2, CN_GI_IT1, CN_GI_IT2, CN_GI_LATE, CN_TRY_IT1, CN_TRY_IT2, CN_WARM_TRY, CN_WARM_OK, CN_WARM_DEP, CN_WARM_NEG, CN_WARM_FULL, CN_ALT_TRY, CN_ALT_HIT,
        ST_K_Y, ST_K_CHK, ST_K_GRAD, ST_K_MU, ST_K_SUB, ST_C_A, ST_C_B, ST_C_Y, ST_C_SQ,
-       ST_SC_COL, ST_SC_ROW, ST_SC_END, ST_L_COEF, ST_L_LOOP };
+       ST_SC_COL, ST_SC_ROW, ST_SC_END, ST_L_COEF, ST_L_LOOP, CN_CYC_HIT, CN_CYC_SKIP };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 constexpr int kMaxNT = 32;         // explicit R^{-1} in GI up to this horizon (WS::useT)
 constexpr int kRepairs = 8;   // also at N = 50: 16 / 32 were no faster in mode 2, 6% / 10% slower in mode 3

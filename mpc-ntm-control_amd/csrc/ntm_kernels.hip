@@ -19,6 +19,7 @@
 #include <string>
 
 #include "ntm_device.h"
+#include "ntm_mixed.h"
 
 using namespace ntm;
 
@@ -104,6 +105,13 @@ __device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x
                             int64_t B = 0, int64_t s = 0) {
     int flag = NTM_EXIT_OPTIMAL, it;
     int n_qp = 0, n_gi = 0, n_act = 0, n_gen = 0, n_try = 0, n_girun = 0;
+#ifdef NTM_STAMPS
+    // exact 2-cycle study (diagnostic build): is the state after iteration it
+    // (rho and U) bit-identical to the state after iteration it-2?  A necessary
+    // condition for the LPV loop to repeat exactly from there on
+    double cr[2][3] = {{0, 0, 0}, {0, 0, 0}}, cu[2] = {0, 0};
+    int cyc = 0;
+#endif
     for (it = 1; it <= pb.i_sim; ++it) {
         int qi = 0, qa = 0, ns = 0;
         flag = qp_phase<P>(pb, w, x0, x1, l, &qi, &qa, &ns, (it - 1) & 1, &n_try, &n_girun, it);
@@ -114,6 +122,21 @@ __device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x
         NTM_T0(tr);
         bool conv = rollout_phase<P>(pb, w, x0, x1, l);
         NTM_ACC(ST_ROLL, tr);
+#ifdef NTM_STAMPS
+        {
+            double r0 = 0.0, r1 = 0.0, r2 = 0.0, u = 0.0;
+            if (l < w.n()) { r0 = w.rho()[3 * l]; r1 = w.rho()[3 * l + 1]; r2 = w.rho()[3 * l + 2]; u = w.U()[l]; }
+            const int sl = it & 1;
+            int ne = (it < 3) || (l < w.n() && (r0 != cr[sl][0] || r1 != cr[sl][1] || r2 != cr[sl][2] || u != cu[sl]));
+            ne = gmaxi<P>(ne);
+            if (!ne && !cyc) {
+                cyc = it;
+                NTM_CNT(CN_CYC_HIT);
+                if ((threadIdx.x & 63) == 0) ntm_lds_stamps[CN_CYC_SKIP] += (unsigned long long)(pb.i_sim - it);
+            }
+            cr[sl][0] = r0; cr[sl][1] = r1; cr[sl][2] = r2; cu[sl] = u;
+        }
+#endif
         if (conv) break;
     }
     *iters = it > pb.i_sim ? pb.i_sim : it;
@@ -429,6 +452,88 @@ __global__ __launch_bounds__(64) void k_qp(int64_t B, int N, int m, const double
     if (l == 0) {
         exitflag[s] = flag;
         if (iters) iters[s] = its;
+    }
+}
+
+// Mixed precision (BASELINE config 5's fp32 leg; not the fp64 product path):
+// the QP solved by Goldfarb-Idnani in fp32 on fp32-rounded data (ntm_mixed.h),
+// then its active set re-solved exactly in fp64 and KKT-certified (the fp64
+// path's polish); when the fp32 set does not certify, the fp64 GI solves it.
+// info bits: 1 = the fp32 active set certified in fp64, 2 = fp64 GI fallback,
+// 4 = the fp32 solve itself ended non-optimal.
+template <int P>
+__global__ __launch_bounds__(64) void k_qp_mixed(int64_t B, int N, int m, const double* G_in, const double* F_in,
+                                                 const double* Lin, const double* b, double* U, double* U32,
+                                                 int32_t* exitflag, int32_t* info, int32_t* iters32) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int l = threadIdx.x;
+    const int64_t s = blockIdx.x;
+    if (s >= B) return;
+    const int wsm = ws_bytes_rows(N, m);
+    char* base = smem;
+    auto w = ws_carve<0>(base, N);
+    double* rnrm = reinterpret_cast<double*>(base + wsm);
+    double* gsave = rnrm + ((m + 1) & ~1);
+    char* b32 = reinterpret_cast<char*>(gsave + N * ldj_of(N));
+    GI32 g;
+    g.carve(b32, N, m);
+    // ---- fp32 stage
+    int q32 = 0, it32 = 0;
+    const Dense32 r32{Lin, b, s, N, m};
+    const int f32 = gi32_solve<P>(g, G_in, F_in, r32, s, l, &q32, &it32);
+    // ---- fp64 data (as k_qp)
+    if (l < N) {
+        for (int kk = 0; kk <= l; ++kk) w.R()[l + kk * w.ldj()] = G_in[s * (N * N) + l + kk * N];
+        w.F()[l] = F_in[s * N + l];
+    }
+    for (int i = l; i < m; i += P) w.aflag()[i] = 0;
+    NTM_WSYNC();
+    int flag, its = 0, q = 0, inf = (f32 != NTM_EXIT_OPTIMAL) ? 4 : 0;
+    DenseRows rows{Lin, b, rnrm, (int64_t)N, s, m};
+    if (!scale_phase<P>(w, l, false)) {
+        flag = NTM_EXIT_NONFINITE;
+    } else {
+        const int code = rows.template prepare_code<P>(w, l);
+        if (code & 1) flag = NTM_EXIT_NONFINITE;
+        else if (code & 2) flag = NTM_EXIT_INFEASIBLE;
+        else {
+            if (l < N) for (int j = 0; j <= l; ++j) gsave[l + j * w.ldj()] = w.R()[l + j * w.ldj()];
+            NTM_WSYNC();
+            bool ok = false;
+            if (f32 == NTM_EXIT_OPTIMAL) {
+                // ---- fp64 refinement on the fp32 active set
+                if (l < q32) w.act()[l] = g.act[l];
+                if (l < N) w.V()[l] = (double)g.U[l] / w.D()[l];
+                NTM_WSYNC();
+                ok = polish_phase<P, DenseRows, decltype(w)>(Prob{}, w, &rows, q32, l, gsave, false, false, nullptr);
+                NTM_WSYNC();
+            }
+            if (ok) {
+                flag = NTM_EXIT_OPTIMAL;
+                inf |= 1;
+            } else {
+                // ---- fp64 Goldfarb-Idnani fallback (G~ restored from the saved copy)
+                inf |= 2;
+                if (l < N) for (int j = 0; j <= l; ++j) w.R()[l + j * w.ldj()] = gsave[l + j * w.ldj()];
+                for (int i = l; i < m; i += P) w.aflag()[i] = 0;
+                NTM_WSYNC();
+                flag = gi_solve<P, DenseRows, decltype(w)>(w, rows, m > 0, m, l, &its, &q);
+                if (flag == NTM_EXIT_OPTIMAL)
+                    (void)polish_phase<P, DenseRows, decltype(w)>(Prob{}, w, &rows, q, l, gsave, false, false,
+                                                                  nullptr);
+            }
+        }
+    }
+    if (flag != NTM_EXIT_OPTIMAL && l < N) w.U()[l] = (flag == NTM_EXIT_MAXITER) ? w.V()[l] * w.D()[l] : 0.0;
+    NTM_WSYNC();
+    if (l < N) {
+        U[s * N + l] = w.U()[l];
+        U32[s * N + l] = (double)g.U[l];
+    }
+    if (l == 0) {
+        exitflag[s] = flag;
+        info[s] = inf;
+        iters32[s] = it32;
     }
 }
 
@@ -1045,7 +1150,7 @@ int ntm_qp_device(ntm_ctx* ctx, int64_t B, int32_t N, int32_t m, const double* G
     DeviceGuard dg(ctx);
     if (!ctx) return NTM_E_INVALID;
     if (N < 1 || N > NTM_MAX_N) return fail(ctx, NTM_E_INVALID, "N out of range [1, 64]");
-    if (m < 0 || m > 6 * NTM_MAX_N + 4) return fail(ctx, NTM_E_INVALID, "m out of range");
+    if (m < 0 || m > 8 * NTM_MAX_N + 4) return fail(ctx, NTM_E_INVALID, "m out of range");
     if (B < 0) return fail(ctx, NTM_E_INVALID, "negative batch");
     if (B == 0) return NTM_OK;
     if (!G || !F || !U || !exitflag) return fail(ctx, NTM_E_INVALID, "null array");
@@ -1067,6 +1172,25 @@ int ntm_qp_device(ntm_ctx* ctx, int64_t B, int32_t N, int32_t m, const double* G
         hipLaunchKernelGGL((k_qp<64, 0>), dim3(blocks), dim3(64), lds, st, B, N, m, G, F, Lin, b, U, exitflag, iters);
     }
     return check_hip(ctx, hipGetLastError(), "k_qp");
+}
+
+int ntm_qp_mixed_device(ntm_ctx* ctx, int64_t B, int32_t N, int32_t m, const double* G, const double* F,
+                        const double* Lin, const double* b, double* U, double* U32, int32_t* exitflag,
+                        int32_t* info, int32_t* iters32, void* stream) {
+    DeviceGuard dg(ctx);
+    if (!ctx) return NTM_E_INVALID;
+    if (N < 1 || N > NTM_MAX_N) return fail(ctx, NTM_E_INVALID, "N out of range [1, 64]");
+    if (m < 0 || m > 8 * NTM_MAX_N + 4) return fail(ctx, NTM_E_INVALID, "m out of range");
+    if (B < 0) return fail(ctx, NTM_E_INVALID, "negative batch");
+    if (B == 0) return NTM_OK;
+    if (!G || !F || !U || !U32 || !exitflag || !info || !iters32) return fail(ctx, NTM_E_INVALID, "null array");
+    if (m > 0 && (!Lin || !b)) return fail(ctx, NTM_E_INVALID, "m > 0 needs Lin and b");
+    size_t lds = (size_t)ws_bytes_rows(N, m) + ((m * 8 + 15) & ~15) + (size_t)N * ldj_of(N) * 8 + GI32::bytes(N, m);
+    int rc;
+    if ((rc = set_lds(ctx, k_qp_mixed<64>, lds))) return rc;
+    hipLaunchKernelGGL((k_qp_mixed<64>), dim3((unsigned)B), dim3(64), lds, (hipStream_t)stream, B, N, m, G, F, Lin, b,
+                       U, U32, exitflag, info, iters32);
+    return check_hip(ctx, hipGetLastError(), "k_qp_mixed");
 }
 
 // splitmix64-based counter generator (identical to oracle/ntm_oracle.py scenario_x0)

@@ -80,6 +80,8 @@ EXPORTS = {
     "ntm_cost_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _V, _V, _V, _V, _V]),
     "ntm_getwlc_device": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _V, _V, _V, _V, _V]),
     "ntm_qp_device": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, _V, _V, _V, _V, _V, _V, _V, _V]),
+    "ntm_qp_mixed_device": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_int32, _V, _V, _V, _V, _V, _V, _V,
+                                      _V, _V, _V]),
     "ntm_scenarios_x0": (None, [C.c_uint64, C.c_int64, C.c_int64, _DP]),
     "ntm_ctx_set_scenarios": (C.c_int, [C.c_void_p, C.POINTER(NtmScenarioGen)]),
     "ntm_scenario_sample": (None, [C.POINTER(NtmScenarioGen), C.c_int64, C.c_int32, _DP]),

@@ -459,6 +459,30 @@ class NtmMpc:
         return U, flag, its
 
 
+def _quadprog_mixed(self, H: torch.Tensor, f: torch.Tensor, Lin: torch.Tensor | None, b: torch.Tensor | None):
+    """Config 5's fp32 leg (ntm_qp_mixed_device; not the fp64 product path): the QP
+    solved in fp32 on fp32-rounded data, its active set then re-solved exactly in
+    fp64 and certified (fp64 fallback otherwise).  Returns (U refined (N, B),
+    U32 fp32 solution (N, B), exitflag (B,), info (B,) bit 0 certified / bit 1
+    fp64 fallback / bit 2 fp32 not optimal, fp32 GI iterations (B,))."""
+    N, Bn = f.shape
+    m = 0 if Lin is None else b.shape[0]
+    H, _ = _dev_arg(H, (N * N, Bn), name="H")
+    f, _ = _dev_arg(f, (N, Bn), name="f")
+    if m:
+        Lin, _ = _dev_arg(Lin, (m * N, Bn), name="A")
+        b, _ = _dev_arg(b, (m, Bn), name="b")
+    U, U32 = self._empty(N, Bn), self._empty(N, Bn)
+    flag, info, its = (self._empty(Bn, dtype=torch.int32) for _ in range(3))
+    self._raise(self.lib.ntm_qp_mixed_device(self._ctx, Bn, N, m, _ptr(H), _ptr(f), _ptr(Lin) if m else None,
+                                             _ptr(b) if m else None, _ptr(U), _ptr(U32), _ptr(flag), _ptr(info),
+                                             _ptr(its), self._stream()), "ntm_qp_mixed_device")
+    return U, U32, flag, info, its
+
+
+NtmMpc.quadprog_mixed = _quadprog_mixed
+
+
 def scenarios_x0(first_id: int, B: int, seed: int = 20241220):
     """Synthetic initial states for global ids first_id..first_id+B-1:
     (2, B) float64 numpy array in the ABI layout (each scenario's [w, omega] contiguous)."""

@@ -138,3 +138,23 @@ def test_run_vs_closed_loop_fixture(ctl, name):
     wpr = wp.reshape(k_sim, N + 1, S).transpose(2, 0, 1)          # fixture: (S, k_sim, N + 1)
     assert np.max(np.abs(wpr - d["wpred"])) <= tol * 0.15
     assert (its.T == d["inner_iters"]).mean() >= 0.9
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_quadprog_mixed_vs_certified_optimum(ctl, mode):
+    """Config 5's fp32 leg (ntm_qp_mixed_device): the fp32 solve on fp32-rounded
+    data lands within fp32 accuracy of the certified optimum, and the fp64
+    refinement of its active set (fp64 fallback when it does not certify)
+    recovers the optimum to the fp64 bound, 1e-10 * umax."""
+    d = np.load(GOLD / f"qp_m{mode}_N20.npz")
+    n = d["G"].shape[0]
+    Gb = np.stack([d["G"][i].reshape(-1, order="F") for i in range(n)], axis=1)
+    Lb = np.stack([d["Lin"][i].reshape(-1, order="F") for i in range(n)], axis=1)
+    U, U32, flag, info, _ = ctl.quadprog_mixed(T(Gb), T(d["F"].T), T(Lb), T(d["b"].T))
+    U, U32, flag, info = H(U), H(U32), H(flag), H(info)
+    np.testing.assert_array_equal(flag, d["exitflag"])
+    err = np.max(np.abs(U - d["U_exact"].T)) / 2e6
+    e32 = np.max(np.abs(U32 - d["U_exact"].T)) / 2e6
+    print(f"mode {mode}: mixed {err:.3e}, fp32 {e32:.3e}, certified {np.mean(info & 1):.2f}")
+    assert err <= 1e-10, err
+    assert e32 <= 1e-2, e32                  # fp32: ~1e-7 .. 1e-3 of umax (DESIGN §6)

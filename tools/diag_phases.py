@@ -47,3 +47,5 @@ fine = "k_y k_chk k_grad k_mu k_sub c_a c_b c_y c_sq sc_col sc_row sc_end l_coef
 print("certificate / classification detail, cycles per wave-step:")
 for i, n in enumerate(fine):
     print(f"  {n:9s} {buf[46 + i]/B:12.0f}")
+print(f"exact 2-cycle study: steps whose rho and U after iteration it equal those after it-2 (it >= 3): "
+      f"{buf[60]/B:.4f} per wave-step; iterations a shortcut could skip {buf[61]/B:.4f} per wave-step")
