@@ -264,7 +264,7 @@ def main():
     import ntm_mpc
     from ntm_mpc import Config, NtmMpc, ScenarioGen
     from ntm_mpc import flops as FL
-    from ntm_mpc.dist import gather_scenarios
+    from ntm_mpc.dist import gather_to_root
 
     B, N, K, W = args.batch, args.N, args.steps, args.warmup
     cfg = Config(N=N, mode=args.mode)
@@ -273,12 +273,13 @@ def main():
     x0 = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(rank * B, B), local)
 
     leg = _run_leg(ctl, cfg, B, K, W, x0, rank, world, collect=True, stats_on=not args.no_stats)
-    # end-of-batch gather of every per-scenario output history (RCCL over xGMI;
-    # gloo rehearsal through host memory), scenario order = global id order
+    # end-of-batch gather of every per-scenario output history into rank 0 (RCCL
+    # point-to-point over xGMI; gloo rehearsal through host memory), scenario
+    # order = global id order
     g = None
     if world > 1:
         tot = world * B
-        g = {k: gather_scenarios(v.cpu() if rehearsal else v, tot) for k, v in leg["hist"].items()}
+        g = {k: gather_to_root(v.cpu() if rehearsal else v, tot) for k, v in leg["hist"].items()}
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -288,7 +289,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     r = _finish_leg(ctl, leg, K)
-    if g is None:
+    if world == 1:
         g = leg["hist"]
     verify = None
     if rank == 0 and args.verify > 0:
@@ -328,8 +329,8 @@ def main():
         "config": {"workload": _workload(N, args.mode, B),
                    "scenarios_per_gpu": B, "global_batch": world * B, "N": N, "mode": args.mode, "i_sim": 10,
                    "timed_closed_loop_steps": f"{W + 1}-{W + K}",
-                   "parallelism": f"scenario-sharded x{world} (weak), end-of-batch gather of uk, Uk, xk, wpred, "
-                                  "exitflag, inner_iters"
+                   "parallelism": f"scenario-sharded x{world} (weak), end-of-batch gather into rank 0 of uk, Uk, xk, "
+                                  "wpred, exitflag, inner_iters"
                        + (" [gloo rehearsal: ranks share devices]" if rehearsal and world > 1 else "")},
         "roofline": {"bound": "valu-fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,

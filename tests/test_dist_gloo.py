@@ -37,13 +37,19 @@ def _worker(rank, world, port, total, out_path):
     uk = gather_scenarios(torch.from_numpy(res["uk"]), total)
     xk = gather_scenarios(torch.from_numpy(res["xk"]), total)
     fl = gather_scenarios(torch.from_numpy(res["exitflag"]), total)
+    from ntm_mpc.dist import gather_to_root
+    roots = {k: gather_to_root(torch.from_numpy(np.ascontiguousarray(res[k])), total)
+             for k in ("uk", "Uk", "xk", "wpred", "exitflag", "inner_iters")}
+    if rank != 0:
+        assert all(v is None for v in roots.values())
     if rank == 0:
-        np.savez(out_path, uk=uk.numpy(), xk=xk.numpy(), fl=fl.numpy())
+        np.savez(out_path, uk=uk.numpy(), xk=xk.numpy(), fl=fl.numpy(),
+                 **{"root_" + k: v.numpy() for k, v in roots.items()})
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,total", [(2, 13), (2, 8)])
+@pytest.mark.parametrize("world,total", [(2, 13), (2, 8), (3, 10)])
 def test_sharded_gather_equals_single_process(tmp_path, world, total):
     out = tmp_path / "g.npz"
     mp.spawn(_worker, args=(world, _free_port(), total, str(out)), nprocs=world, join=True)
@@ -54,6 +60,8 @@ def test_sharded_gather_equals_single_process(tmp_path, world, total):
     np.testing.assert_array_equal(g["uk"], ref["uk"])        # bitwise: scenarios are independent
     np.testing.assert_array_equal(g["xk"], ref["xk"])
     np.testing.assert_array_equal(g["fl"], ref["exitflag"])
+    for k in ("uk", "Uk", "xk", "wpred", "exitflag", "inner_iters"):          # gather to rank 0 only
+        np.testing.assert_array_equal(g["root_" + k], ref[k], err_msg=k)
 
 
 def test_shard_range_partitions():

@@ -632,3 +632,61 @@ def test_full_size_batch_properties(ctl, N, mode):
     sub = ctl.step(T(xs), T(rs), T(us), cfg, active_ws=ws[:, ids].contiguous())
     for k in ("U", "x_pred", "x_next", "exitflag", "inner_iters"):
         np.testing.assert_array_equal(H(sub[k]), H(out[k])[..., ids], err_msg=k)
+
+
+def _one_collision(Lin, act, N):
+    """Does the active set have the long-horizon 'one collision' shape:
+    as many general rows as free variables, and exactly one free column in which
+    no general row ends (two rows end in the same one)?"""
+    nz = [np.nonzero(np.abs(Lin[r]) > 0)[0] for r in act]
+    fixed = {int(c[0]) for c in nz if len(c) == 1}
+    free = [j for j in range(N) if j not in fixed]
+    gen = [c for c in nz if len(c) > 1]
+    if len(gen) != len(free) or not gen:
+        return False
+    last = [max(j for j in c if j not in fixed) if any(j not in fixed for j in c) else -1 for c in gen]
+    holes = [j for j in free if j not in last]
+    return len(holes) == 1 and -1 not in last
+
+
+def test_long_horizon_sets_vs_exact_kkt(ctl):
+    """the N=50 re-solve paths (echelon k = 0 / 1, the one-collision
+    echelon set of config 5, the bordered elimination) checked against an exact
+    (30-digit) KKT solve of the SAME active set the device certified.  One QP per
+    launch (i_sim = 1) so the QP's data are the launch inputs; the device's
+    active set is read back from its warm-start workspace.  The exact solve must
+    certify the set (primal feasible, multipliers >= 0) and the device's U must
+    match it to 1e-10 * umax; at least one set must be a one-collision set."""
+    N, B, steps = 50, 8, 4
+    cfg, ocfg = cfgs(N, 3, i_sim=1)
+    ph = O.Physics()
+    x = O.scenario_x0(np.arange(B)).T
+    rho, Uo = cbind.initial_state(x, ocfg)
+    ws = ctl.new_active_ws(B, cfg)
+    n_coll = n_checked = 0
+    worst = 0.0
+    for k in range(steps):
+        tr, tu = T(rho), T(Uo)
+        out = ctl.step(T(x), tr, tu, cfg, active_ws=ws)
+        U, flag, wsh = H(out["U"]), H(out["exitflag"]), H(ws)
+        for s in range(B):
+            if flag[s] != 1:
+                continue
+            q = int(wsh[N, s])                              # slot 0: the launch's one QP
+            act = [int(v) for v in wsh[:q, s]]
+            Rho = rho[:, s].reshape(N, 3).T
+            Phi, Gam, Lam = O.lift(Rho, ph, ocfg)
+            G, F = O.cost(Phi, Gam, Lam, x[:, s], ocfg)
+            Lin, b = O.constraints(Phi, Gam, Lam, x[:, s], ocfg)
+            if k >= 2 and n_checked >= 12 and not _one_collision(Lin, act, N):
+                continue                                    # keep the mpmath work bounded
+            Ue, lam, cert = O.kkt_polish(G, F, Lin, b, act, dps=30)
+            assert cert["max_violation"] <= 1e-9, (k, s, cert)
+            assert cert["min_multiplier"] >= -1e-9 * max(1.0, np.max(np.abs(lam))), (k, s, cert)
+            worst = max(worst, np.max(np.abs(U[:, s] - Ue)) / cfg.umax)
+            n_checked += 1
+            n_coll += _one_collision(Lin, act, N)
+        x, rho, Uo = H(out["x_next"]), H(tr), H(tu)         # the device's own closed loop
+    print(f"N=50 mode 3: {n_checked} sets checked, {n_coll} one-collision, max |U - U_exact| / umax = {worst:.2e}")
+    assert n_checked >= 8 and n_coll >= 1
+    assert worst <= 1e-10, worst
