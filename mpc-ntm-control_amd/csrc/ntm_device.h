@@ -194,6 +194,21 @@ constexpr double kConstTol = 1e-9;
 constexpr int kRowMulti = 256;     // WS::rinfo flag: the state row has two or more non-zeros
 constexpr int kGiWarmRejected = 100;   // gi_solve: the warm-start set was not dual feasible (caller reruns cold)
 
+// Terms per batch of the LDS contractions (loads issued ahead of their uses);
+// a translation unit may set its own (ntm_n50.hip)
+#ifndef NTM_CH
+#define NTM_CH 4
+#endif
+// Unroll count of the CH-batched chunk loops: empty (the compiler's choice, full
+// unrolling at the BASELINE horizons) unless a build sets NTM_CHUNK_UNROLL
+#define NTM_STR_(x) #x
+#define NTM_STR(x) NTM_STR_(x)
+#ifdef NTM_CHUNK_UNROLL
+#define NTM_CHUNK_PRAGMA _Pragma(NTM_STR(unroll NTM_CHUNK_UNROLL))
+#else
+#define NTM_CHUNK_PRAGMA
+#endif
+
 #define NTM_WSYNC()                                              \
     do {                                                         \
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   \
@@ -511,6 +526,7 @@ template <int CH>
 __device__ __forceinline__ double qdot_rows(const double* a, const double* b, int n, int imin, double q00,
                                             double q01, double q10, double q11) {
     double s = 0.0;
+    NTM_CHUNK_PRAGMA
     for (int i0 = 0; i0 < n; i0 += CH) {
         double a0[CH], a1[CH], b0[CH], b1[CH];
 #pragma unroll
@@ -538,6 +554,7 @@ __device__ __forceinline__ double qdot_rows(const double* a, const double* b, in
 template <int CH>
 __device__ __forceinline__ double dot_batched(const double* a, int sa, const double* b, int sb, int n) {
     double y = 0.0;
+    NTM_CHUNK_PRAGMA
     for (int j0 = 0; j0 < n; j0 += CH) {
         double x[CH], z[CH];
 #pragma unroll
@@ -557,6 +574,7 @@ __device__ __forceinline__ double dot_batched(const double* a, int sa, const dou
 template <int CH>
 __device__ __forceinline__ double dot_range(const double* a, int sa, const double* b, int sb, int lo, int hi) {
     double y = 0.0;
+    NTM_CHUNK_PRAGMA
     for (int j0 = lo; j0 < hi; j0 += CH) {
         double x[CH], z[CH];
 #pragma unroll
@@ -575,6 +593,7 @@ __device__ __forceinline__ double dot_range(const double* a, int sa, const doubl
 // s - sum_{lo <= j < hi} a[j sa] b[j sb], the terms subtracted one by one in index order
 template <int CH>
 __device__ __forceinline__ double sub_dot(double s, const double* a, int sa, const double* b, int sb, int lo, int hi) {
+    NTM_CHUNK_PRAGMA
     for (int j0 = lo; j0 < hi; j0 += CH) {
         double x[CH], z[CH];
 #pragma unroll
@@ -593,6 +612,7 @@ __device__ __forceinline__ double sub_dot(double s, const double* a, int sa, con
 // a[j] -= f b[j] for lo <= j < hi, the loads of CH entries issued ahead of their stores
 template <int CH>
 __device__ __forceinline__ void axpy_sub(double* a, const double* b, double f, int lo, int hi) {
+    NTM_CHUNK_PRAGMA
     for (int j0 = lo; j0 < hi; j0 += CH) {
         double x[CH], z[CH];
 #pragma unroll
@@ -614,6 +634,7 @@ __device__ __forceinline__ double gamma_row_dot(const W& w, int r, const double*
     const int n = w.n(), jm = r >> 1;
     const double* gr = w.Gt() + r;                        // gt(r, j) = gr[gidx(0, j)]
     double y = 0.0;
+    NTM_CHUNK_PRAGMA
     for (int j0 = 0; j0 < n; j0 += CH) {
         double g[CH], x[CH];
 #pragma unroll
@@ -641,6 +662,7 @@ __device__ __forceinline__ void gamma_row_dot2(const W& w, int r, const double* 
     const double* gr = w.Gt() + r;
     y1 = 0.0;
     y2 = 0.0;
+    NTM_CHUNK_PRAGMA
     for (int j0 = 0; j0 < n; j0 += CH) {
         double g[CH], x1[CH], x2[CH];
 #pragma unroll
@@ -763,7 +785,8 @@ __device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l) {
         // rewrite the diagonal.  The coefficients of CH steps are loaded ahead of the
         // chunk's stores (the stores cannot be proven not to alias them, so per-step
         // loads would wait for the previous step's stores: one LDS round trip a step)
-        constexpr int CH = 4;
+        constexpr int CH = NTM_CH;
+        NTM_CHUNK_PRAGMA
         for (int i0 = 1; i0 < N; i0 += CH) {
             double ca[CH], cb[CH];
 #pragma unroll
@@ -834,6 +857,7 @@ __device__ __forceinline__ void free_response(const W& w, double x0, double x1, 
 template <int CH>
 __device__ __forceinline__ double dot_rows2(const double* a, const double* c, int n, int imin) {
     double s = 0.0;
+    NTM_CHUNK_PRAGMA
     for (int i0 = 0; i0 < n; i0 += CH) {
         double a0[CH], a1[CH], c0[CH], c1[CH];
 #pragma unroll
@@ -940,7 +964,8 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
         const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
         const double* om = w.xp();               // Om (e_i - r), from free_response
         double s = 0.0, fs = 0.0;
-        constexpr int CH = 4;
+        constexpr int CH = NTM_CH;
+        NTM_CHUNK_PRAGMA
         for (int i0 = 0; i0 < N; i0 += CH) {     // fixed trip count, terms i < l masked; batched loads
             double ga[CH], gb[CH], ea[CH], eb[CH];
 #pragma unroll
@@ -988,7 +1013,8 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
             double s = 0.0;
             const int jmax = r >> 1;
             int last = -1, cnt = 0;
-            constexpr int CH = 4;
+            constexpr int CH = NTM_CH;
+            NTM_CHUNK_PRAGMA
             for (int j0 = 0; j0 < N; j0 += CH) { // fixed trip count, j > jmax masked; batched loads
                 double g[CH], dd[CH];
 #pragma unroll
@@ -1219,7 +1245,7 @@ struct StructRows {
                         // fixed trip count, entries j > jmax masked.  The packed reads stay
                         // inside Gt: gidx(0, j) + r = j(2N-j-1) + r < N(N+1)
                         (void)gr;
-                        xh = gamma_row_dot<4>(w, r, w.U());
+                        xh = gamma_row_dot<NTM_CH>(w, r, w.U());
                     }
                     const double er = w.e()[r];
                     xh += er;
@@ -1337,7 +1363,7 @@ __device__ __forceinline__ bool chol_inplace(double* A, int n, int RS, int CS, i
     for (int k = 0; k < n; ++k) {
         double s = 0.0;
         if (l >= k && l < n) {
-            s = sub_dot<4>(A[l * RS + k * CS], A + l * RS, CS, A + k * RS, CS, 0, k);
+            s = sub_dot<NTM_CH>(A[l * RS + k * CS], A + l * RS, CS, A + k * RS, CS, 0, k);
         }
         double dk = gbcast<P>(s, k);
         if (!(dk > 0.0) || !(dk < kInf)) return false;
@@ -1395,7 +1421,7 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
         for (int i = 0; i < N; ++i) {
             double x = 0.0;
             if (i >= l) {
-                x = sub_dot<4>((i == l) ? 1.0 : 0.0, w.R() + i, LD, w.J() + l * LDJ, 1, l, i);
+                x = sub_dot<NTM_CH>((i == l) ? 1.0 : 0.0, w.R() + i, LD, w.J() + l * LDJ, 1, l, i);
                 x *= w.ldi()[i];
             }
             w.J()[l * LDJ + i] = x;
@@ -1406,11 +1432,11 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
     double Vl = 0.0;
     {
         double t = 0.0;
-        if (l < N) t = dot_batched<4>(w.J() + l, LDJ, w.F(), 1, N);
+        if (l < N) t = dot_batched<NTM_CH>(w.J() + l, LDJ, w.F(), 1, N);
         if (l < N) w.d()[l] = t;
         NTM_WSYNC();
         if (l < N) {
-            const double v = dot_batched<4>(w.J() + l * LDJ, 1, w.d(), 1, N);
+            const double v = dot_batched<NTM_CH>(w.J() + l * LDJ, 1, w.d(), 1, N);
             Vl = -v;
             w.V()[l] = Vl;
             w.U()[l] = w.D()[l] * Vl;
@@ -1450,12 +1476,12 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
                 if (l < N) dl = esg * w.J()[ej * LDJ + l];
             } else {
                 bcp = uni<P>(rows.template load_np<P>(w, p, l));
-                if (l < N) dl = dot_batched<4>(w.J() + l, LDJ, w.np(), 1, N);
+                if (l < N) dl = dot_batched<NTM_CH>(w.J() + l, LDJ, w.np(), 1, N);
             }
             if (l < N) { w.d()[l] = (l >= q) ? dl : 0.0; w.dr()[l] = (l < q) ? dl : 0.0; }
             NTM_WSYNC();
             double rl = 0.0;
-            if (useT && l < N) rl = dot_batched<4>(w.T() + l * LDJ, 1, w.dr(), 1, N);
+            if (useT && l < N) rl = dot_batched<NTM_CH>(w.T() + l * LDJ, 1, w.dr(), 1, N);
             const double zn = gsum<P>((l >= q && l < N) ? dl * dl : 0.0);
             const double dnrm = gsum<P>(dl * dl);
             if (q >= N) { NTM_CNT(CN_WARM_FULL); break; }
@@ -1474,9 +1500,9 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
                 double vtv = gsum<P>(vl * vl);
                 NTM_WSYNC();
                 if (l < N) {
-                    const double dot = dot_batched<4>(w.J() + l * LDJ, 1, w.hv(), 1, N);
+                    const double dot = dot_batched<NTM_CH>(w.J() + l * LDJ, 1, w.hv(), 1, N);
                     const double f = 2.0 * dot / vtv;
-                    axpy_sub<4>(w.J() + l * LDJ, w.hv(), f, q, N);
+                    axpy_sub<NTM_CH>(w.J() + l * LDJ, w.hv(), f, q, N);
                 }
             }
             const double ih = 1.0 / h;
@@ -1497,9 +1523,9 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
         if (okw) {
             // c = J' F~ (lane k), wv = (T' bc)_k for k < q
             double c = 0.0, wv = 0.0;
-            if (l < N) c = dot_batched<4>(w.J() + l, LDJ, w.F(), 1, N);
+            if (l < N) c = dot_batched<NTM_CH>(w.J() + l, LDJ, w.F(), 1, N);
             if (useT) {
-                if (l < q) wv = dot_range<4>(w.T() + l, LDJ, w.Vb(), 1, 0, l + 1);
+                if (l < q) wv = dot_range<NTM_CH>(w.T() + l, LDJ, w.Vb(), 1, 0, l + 1);
             } else {                                 // long horizons: R' wv = bc by forward substitution
                 double acc = (l < q) ? w.Vb()[l] : 0.0;
                 for (int k2 = 0; k2 < q; ++k2) {
@@ -1517,7 +1543,7 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
             double v = 0.0, u = 0.0;
             if (l < N) for (int k2 = 0; k2 < N; ++k2) v += w.J()[l * LDJ + k2] * (w.dr()[k2] - w.d()[k2]);
             if (useT) {
-                if (l < q) u = dot_range<4>(w.T() + l * LDJ, 1, w.np(), 1, l, q);
+                if (l < q) u = dot_range<NTM_CH>(w.T() + l * LDJ, 1, w.np(), 1, l, q);
             } else {                                 // R u = wv + c1 by back substitution
                 double acc = (l < q) ? w.np()[l] : 0.0;
                 for (int b = q - 1; b >= 0; --b) {
@@ -1583,7 +1609,7 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
             if (ej >= 0) {
                 if (l < N) dl = esg * w.J()[ej * LDJ + l];
             } else if (l < N) {
-                dl = dot_batched<4>(w.J() + l, LDJ, w.np(), 1, N);
+                dl = dot_batched<NTM_CH>(w.J() + l, LDJ, w.np(), 1, N);
             }
             // d split at q: d2 = d[q:N] (w.d) and d1 = d[0:q] (w.dr), zero elsewhere, so
             // both matvecs run full fixed-length rows (unrolled, loads batched)
@@ -1592,8 +1618,8 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
             // z = J2 d2 (primal direction) and r = T d1 = R^{-1} d1 (negative dual direction)
             double zl = 0.0, rl = 0.0;
             if (l < N) {
-                zl = dot_batched<4>(w.J() + l * LDJ, 1, w.d(), 1, N);
-                if (useT) rl = dot_batched<4>(w.T() + l * LDJ, 1, w.dr(), 1, N);
+                zl = dot_batched<NTM_CH>(w.J() + l * LDJ, 1, w.d(), 1, N);
+                if (useT) rl = dot_batched<NTM_CH>(w.T() + l * LDJ, 1, w.dr(), 1, N);
             }
             if (!useT) {                       // long horizons: back substitution on R
                 double acc = (l < q) ? dl : 0.0;
@@ -1638,9 +1664,9 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
                         double vtv = gsum<P>(vl * vl);
                         NTM_WSYNC();
                         if (l < N) {
-                            const double dot = dot_batched<4>(w.J() + l * LDJ, 1, w.hv(), 1, N);
+                            const double dot = dot_batched<NTM_CH>(w.J() + l * LDJ, 1, w.hv(), 1, N);
                             const double f = 2.0 * dot / vtv;
-                            axpy_sub<4>(w.J() + l * LDJ, w.hv(), f, q, N);
+                            axpy_sub<NTM_CH>(w.J() + l * LDJ, w.hv(), f, q, N);
                         }
                     }
                     // R gains column q = [d1; h]; T = R^{-1} gains column q = [-r/h; 1/h]
@@ -2022,7 +2048,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     NTM_WSYNC();
     NTM_ACC(ST_C_B, tp);
     for (int r = l; r < 2 * N; r += P) {
-        const double y = gamma_row_dot<4>(w, r, w.dr());
+        const double y = gamma_row_dot<NTM_CH>(w, r, w.dr());
         w.Phi()[r] = y;
         w.xp()[r] = y + w.e()[r] - ((r & 1) ? pb.r[1] : pb.r[0]);
     }
@@ -2093,7 +2119,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     if (!sq && l < nF) {
         const int ja = w.fidx()[l];
         const double* ca = w.Gt() + w.gidx(2 * ja, ja) - 2 * ja;   // ca[r] = gt(r, ja), r >= 2 ja
-        const double g2 = qdot_rows<4>(ca, w.xp(), N, ja, q00, q01, q10, q11);   // terms i < ja masked
+        const double g2 = qdot_rows<NTM_CH>(ca, w.xp(), N, ja, q00, q01, q10, q11);   // terms i < ja masked
         gl = w.D()[ja] * (2 * g2);
     }
     // Bordered KKT system (fused path): rows 0..nF-1 free variables, nF..nt-1 general
@@ -2121,7 +2147,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             const int ja = w.fidx()[a], jc = w.fidx()[c];            // ja >= jc
             const double* ca = w.Gt() + w.gidx(2 * ja, ja) - 2 * ja;
             const double* cc = w.Gt() + w.gidx(2 * jc, jc) - 2 * jc;
-            const double sg = qdot_rows<4>(ca, cc, N, ja, q00, q01, q10, q11);   // terms i < ja masked
+            const double sg = qdot_rows<NTM_CH>(ca, cc, N, ja, q00, q01, q10, q11);   // terms i < ja masked
             const double gv = (2 * sg) * w.D()[ja] * w.D()[jc];
             if (fused) Lp[idx] = gv;                                  // idx == a(a+1)/2 + c
             else w.R()[a + c * LD] = gv;
@@ -2227,7 +2253,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             NTM_WSYNC();
             for (int r = l; r < 2 * N; r += P) {
                 double ya, yb;
-                gamma_row_dot2<4>(w, r, w.U(), w.d(), ya, yb);
+                gamma_row_dot2<NTM_CH>(w, r, w.U(), w.d(), ya, yb);
                 w.xp()[r] = ya;
                 w.Phi()[r] = yb;                                 // scratch (hs_of is done with it)
             }
@@ -2503,7 +2529,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         NTM_WSYNC();
         // y = Gamma U once, for the primal check (state rows) and the gradient
         if (!y_ready) {
-            for (int r = l; r < 2 * N; r += P) w.xp()[r] = gamma_row_dot<4>(w, r, w.U());
+            for (int r = l; r < 2 * N; r += P) w.xp()[r] = gamma_row_dot<NTM_CH>(w, r, w.U());
             NTM_WSYNC();
         }
         NTM_ACC(ST_K_Y, tp);
@@ -2522,7 +2548,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         double res = 0.0;
         if (l < N) {
             const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;
-            const double g2 = dot_rows2<4>(cl, w.xp(), N, l);   // terms i < l masked
+            const double g2 = dot_rows2<NTM_CH>(cl, w.xp(), N, l);   // terms i < l masked
             res = w.D()[l] * (2 * g2) + w.F()[l];
         }
         NTM_ACC(ST_K_GRAD, tp);
@@ -2573,7 +2599,8 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         if (l < N) {
             const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;   // cl[r] = gt(r, l), r >= 2l
             double sub = 0.0;
-            constexpr int CH = 4;
+            constexpr int CH = NTM_CH;
+            NTM_CHUNK_PRAGMA
             for (int s0 = 0; s0 < nS; s0 += CH) {
                 int rr[CH];
                 double zv[CH], gv[CH];
@@ -2650,7 +2677,8 @@ __device__ __forceinline__ bool rollout_phase(const Prob& pb, const W& w, double
         double y0 = x0, y1 = x1;
         w.xp()[0] = y0;
         w.xp()[1] = y1;
-        constexpr int CH = 4;                   // the loads of CH steps ahead of their stores
+        constexpr int CH = NTM_CH;                   // the loads of CH steps ahead of their stores
+        NTM_CHUNK_PRAGMA
         for (int i0 = 0; i0 < N; i0 += CH) {
             double ca[CH], cb[CH], cc[CH], cu[CH];
 #pragma unroll

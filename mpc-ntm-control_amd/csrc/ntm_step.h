@@ -1,0 +1,257 @@
+// ntm_step.h — the hot-path kernels k_mpc_step / k_mpc_run (one fused launch
+// per MPC time step, or per closed loop, for the whole scenario batch) and
+// their per-scenario helpers.  Included by ntm_kernels.hip and, for the N = 50
+// specialisation, by ntm_n50.hip: a translation unit of its own so that its
+// chunk loops can be built without unrolling (NTM_CHUNK_UNROLL) while the
+// other horizons keep the compiler's choice.  Each group of P lanes runs the
+// complete NTM_MPC_Sim.m:94-130 body for one scenario out of LDS.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ntm_device.h"
+
+namespace {
+
+using namespace ntm;
+
+template <int P, class W>
+__device__ __forceinline__ void load_state(const W& w, int64_t B, int64_t s, const double* rho,
+                                           const double* U_old, int l) {
+    const int N = w.n();
+    const double* rs = rho + s * (3 * N);
+    for (int e = l; e < 3 * N; e += P) w.rho()[e] = rs[e];
+    if (l < N) w.Uold()[l] = U_old[s * N + l];
+    NTM_WSYNC();
+}
+
+__device__ __forceinline__ bool is16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// One scenario's record of n doubles from LDS to HBM.  With a 16-byte aligned
+// destination and an even n, lanes store two doubles each (16-B stores: every
+// request carries whole 16-B granules); otherwise one double per lane.
+template <int P>
+__device__ __forceinline__ void store_record(double* dst, const double* src, int n, int l) {
+    if (is16(dst) && (n & 1) == 0) {
+        for (int e = 2 * l; e < n; e += 2 * P)
+            *reinterpret_cast<double2*>(dst + e) = make_double2(src[e], src[e + 1]);
+    } else {
+        for (int e = l; e < n; e += P) dst[e] = src[e];
+    }
+}
+
+// XCD-aware block order (bijective): blocks are dealt round-robin over the 8
+// XCDs, so block b is given the k-th slot of XCD b%8's contiguous range of
+// scenario blocks.  Neighbouring scenarios share the cache lines at the ends
+// of their (scenario-major) records; this keeps each line's users on one L2.
+__device__ __forceinline__ int64_t xcd_swizzle(int64_t b, int64_t nb) {
+    const int64_t q = nb >> 3, r = nb & 7, x = b & 7, k = b >> 3;
+    return x * q + (x < r ? x : r) + k;
+}
+
+// Warm-start workspace (ntm_mpc_step_ws): the active sets of the previous
+// step's last two QPs, 2 slots x (N ids + count) per scenario, in/out.  It is
+// only a hint (every candidate is re-solved exactly and KKT-certified), but it
+// comes from the caller, so each slot is validated before use: count in
+// [0, N], ids in [0, rows), no repeats; anything else disables the slot.
+template <int P, class W>
+__device__ __forceinline__ void load_candidates(const Prob& pb, const W& w, int64_t B, int64_t s, const int32_t* ws, int l) {
+    const int N = w.n();
+    const int nrows = StructRows(pb).rows();
+    const int32_t* wss = ws + s * (2 * (N + 1));
+    for (int e = l; e < 2 * (N + 1); e += P) w.cand()[e] = wss[e];
+    for (int i = l; i < nrows; i += P) w.aflag()[i] = 0;
+    NTM_WSYNC();
+    for (int slot = 0; slot < 2; ++slot) {
+        int* c = w.cand() + slot * (N + 1);
+        const int q = uni<P>(c[N]);
+        if (q < 0) continue;
+        bool bad = q > N || nrows == 0;
+        if (!bad) {
+            int lb = 0;
+            if (l < q) lb = (c[l] < 0 || c[l] >= nrows) ? 1 : 0;
+            bad = gmaxi<P>(lb) != 0;
+        }
+        if (!bad) {
+            int lb = 0;
+            for (int i = 0; i < q; ++i) {         // lane l < q checks its id against the earlier ones
+                const int ci = c[i];
+                if (l < q && i < l && ci == c[l]) lb = 1;
+            }
+            bad = gmaxi<P>(lb) != 0;
+        }
+        if (bad && l == 0) c[N] = -1;
+        NTM_WSYNC();
+    }
+}
+
+// one MPC step on LDS-resident state; returns exit flag, sets *iters
+template <int P, class W>
+__device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x0, double x1, int l, int* iters,
+                            int64_t B = 0, int64_t s = 0) {
+    int flag = NTM_EXIT_OPTIMAL, it;
+    int n_qp = 0, n_gi = 0, n_act = 0, n_gen = 0, n_try = 0, n_girun = 0;
+#ifdef NTM_STAMPS
+    // exact 2-cycle study (diagnostic build): is the state after iteration it
+    // (rho and U) bit-identical to the state after iteration it-2?  A necessary
+    // condition for the LPV loop to repeat exactly from there on
+    double cr[2][3] = {{0, 0, 0}, {0, 0, 0}}, cu[2] = {0, 0};
+    int cyc = 0;
+#endif
+    for (it = 1; it <= pb.i_sim; ++it) {
+        int qi = 0, qa = 0, ns = 0;
+        flag = qp_phase<P>(pb, w, x0, x1, l, &qi, &qa, &ns, (it - 1) & 1, &n_try, &n_girun, it);
+        ++n_qp;
+        n_gi += qi;
+        n_act += qa;
+        n_gen += ns;
+        NTM_T0(tr);
+        bool conv = rollout_phase<P>(pb, w, x0, x1, l);
+        NTM_ACC(ST_ROLL, tr);
+#ifdef NTM_STAMPS
+        {
+            double r0 = 0.0, r1 = 0.0, r2 = 0.0, u = 0.0;
+            if (l < w.n()) { r0 = w.rho()[3 * l]; r1 = w.rho()[3 * l + 1]; r2 = w.rho()[3 * l + 2]; u = w.U()[l]; }
+            const int sl = it & 1;
+            int ne = (it < 3) || (l < w.n() && (r0 != cr[sl][0] || r1 != cr[sl][1] || r2 != cr[sl][2] || u != cu[sl]));
+            ne = gmaxi<P>(ne);
+            if (!ne && !cyc) {
+                cyc = it;
+                NTM_CNT(CN_CYC_HIT);
+                if ((threadIdx.x & 63) == 0) ntm_lds_stamps[CN_CYC_SKIP] += (unsigned long long)(pb.i_sim - it);
+            }
+            cr[sl][0] = r0; cr[sl][1] = r1; cr[sl][2] = r2; cu[sl] = u;
+        }
+#endif
+        if (conv) break;
+    }
+    *iters = it > pb.i_sim ? pb.i_sim : it;
+    if (pb.stats && l == 0) {
+        pb.stats[s] += n_qp;
+        pb.stats[B + s] += n_gi;
+        pb.stats[2 * B + s] += n_act;
+        pb.stats[3 * B + s] += n_gen;
+        pb.stats[4 * B + s] += n_try;
+        pb.stats[5 * B + s] += n_girun;
+    }
+    return flag;
+}
+
+#ifndef NTM_HOT_WAVES_PER_EU
+#define NTM_HOT_WAVES_PER_EU 2
+#endif
+// Long horizons (NN > 32): the LDS workspace already limits a CU to fewer waves
+// than SIMDs, so the register budget of one wave per SIMD costs no occupancy and
+// removes the spills of the fully unrolled horizon loops.
+#define NTM_WAVES_PER_EU(NN) ((NN) > 32 ? 1 : NTM_HOT_WAVES_PER_EU)
+template <int P, int NN, bool GEN>
+__global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, int64_t B, const double* __restrict__ x_k,
+                                                 double* __restrict__ rho, double* __restrict__ U_old,
+                                                 double* __restrict__ U, double* __restrict__ x_pred,
+                                                 double* __restrict__ x_next, int32_t* __restrict__ exitflag,
+                                                 int32_t* __restrict__ inner_iters, int32_t* __restrict__ active_ws) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int G = 64 / P;
+    const int g = threadIdx.x / P, l = threadIdx.x % P;
+    const int64_t s = xcd_swizzle(blockIdx.x, gridDim.x) * G + g;
+    const int N = NN > 0 ? NN : pb.N;
+    NTM_STAMPS_INIT();
+    NTM_TRACE_SET(s, g, l);
+    if (s >= B) return;
+    auto w = ws_carve<NN, GEN>(smem + g * ws_bytes(N), N);
+#ifdef NTM_POISON
+    // debug build (make poison): the workspace starts as NTM_POISON-valued doubles, so
+    // a read of LDS this launch never wrote shows up as a run-to-run difference
+    // (tools/determinism.py + compare_runs.py; this found the x_0-row read of rinfo[-1])
+    for (int e = l; e < ws_bytes(N) / 8; e += P) w.base[e] = NTM_POISON;
+    NTM_WSYNC();
+#endif
+    const double x0 = x_k[2 * s], x1 = x_k[2 * s + 1];
+    if (active_ws) {
+        load_candidates<P>(pb, w, B, s, active_ws, l);
+    } else if (l < 2) {
+        w.cand()[l * (N + 1) + N] = -1;
+    }
+    load_state<P>(w, B, s, rho, U_old, l);
+    scn_store(pb, w, pb.g.first_id + s, l);           // this scenario's plasma (generator)
+    NTM_WSYNC();
+    int its;
+    int flag = mpc_step_dev<P>(pb, w, x0, x1, l, &its, B, s);
+    // scenario-major outputs: each wave writes its scenario's contiguous records
+    store_record<P>(rho + s * (3 * N), w.rho(), 3 * N, l);
+    store_record<P>(U_old + s * N, w.Uold(), N, l);
+    store_record<P>(U + s * N, w.U(), N, l);
+    store_record<P>(x_pred + s * (2 * (N + 1)), w.xp(), 2 * (N + 1), l);
+    {
+        double n0, n1;
+        plant_step<GEN>(pb, scn_coef(pb, w), x0, x1, w.U()[0], n0, n1, pb.g.first_id + s, pb.g.k0);
+        if (is16(x_next)) {
+            if (l == 0) *reinterpret_cast<double2*>(x_next + 2 * s) = make_double2(n0, n1);
+        } else if (l < 2) {
+            x_next[2 * s + l] = l ? n1 : n0;
+        }
+    }
+    if (l == 0) {
+        exitflag[s] = flag;
+        inner_iters[s] = its;
+    }
+    if (active_ws)
+        for (int e = l; e < 2 * (N + 1); e += P) active_ws[s * (2 * (N + 1)) + e] = w.cand()[e];
+    NTM_STAMPS_FLUSH();
+}
+
+template <int P, int NN>
+__global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_run(Prob pb, int64_t B, int k_sim, const double* __restrict__ x0v,
+                                                double* xk, double* uk, double* Uk, double* wpred,
+                                                int32_t* exitflag, int32_t* inner_iters) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int G = 64 / P;
+    const int g = threadIdx.x / P, l = threadIdx.x % P;
+    const int64_t s = xcd_swizzle(blockIdx.x, gridDim.x) * G + g;
+    const int N = NN > 0 ? NN : pb.N;
+    if (s >= B) return;
+    auto w = ws_carve<NN, true>(smem + g * ws_bytes(N), N);
+    double x0 = x0v[2 * s], x1 = x0v[2 * s + 1];
+    if (l < 2) w.cand()[l * (N + 1) + N] = -1;
+    scn_store(pb, w, pb.g.first_id + s, l);           // this scenario's plasma (generator)
+    NTM_WSYNC();
+    {   // Rho = repmat(rho(x0), 1, N) (NTM_MPC_Sim.m:63-65); Uold = +inf (D14)
+        double r1, r2, r3;
+        rho_eval(scn_coef(pb, w), x0, x1, r1, r2, r3);
+        if (l < N) {
+            w.rho()[3 * l] = r1;
+            w.rho()[3 * l + 1] = r2;
+            w.rho()[3 * l + 2] = r3;
+            w.Uold()[l] = kInf;
+        }
+        NTM_WSYNC();
+    }
+    if (xk && l == 0) { xk[s * 2 * (k_sim + 1)] = x0; xk[s * 2 * (k_sim + 1) + 1] = x1; }
+    for (int kk = 0; kk < k_sim; ++kk) {
+        int its;
+        int flag = mpc_step_dev<P>(pb, w, x0, x1, l, &its, B, s);
+        if (Uk && l < N) Uk[(s * k_sim + kk) * N + l] = w.U()[l];
+        if (wpred) for (int i = l; i <= N; i += P) wpred[(s * k_sim + kk) * (N + 1) + i] = w.xp()[2 * i];
+        double n0, n1;
+        plant_step<true>(pb, scn_coef(pb, w), x0, x1, w.U()[0], n0, n1, pb.g.first_id + s, pb.g.k0 + kk);
+        if (l == 0) {
+            if (uk) uk[s * k_sim + kk] = w.U()[0];
+            if (exitflag) exitflag[s * k_sim + kk] = flag;
+            if (inner_iters) inner_iters[s * k_sim + kk] = its;
+            if (xk) { xk[s * 2 * (k_sim + 1) + 2 * kk + 2] = n0; xk[s * 2 * (k_sim + 1) + 2 * kk + 3] = n1; }
+        }
+        x0 = n0;
+        x1 = n1;
+        NTM_WSYNC();
+    }
+}
+
+}  // namespace
+
+// The N = 50 specialisation lives in ntm_n50.hip (its own translation unit);
+// these launch it (grid of one 64-lane block per scenario, lds bytes each).
+hipError_t ntm_launch_step_n50(const ntm::Prob& pb, int64_t B, const double* x_k, double* rho, double* U_old,
+                               double* U, double* x_pred, double* x_next, int32_t* exitflag, int32_t* inner_iters,
+                               int32_t* active_ws, size_t lds, hipStream_t st);
+hipError_t ntm_launch_run_n50(const ntm::Prob& pb, int64_t B, int k_sim, const double* x0, double* xk, double* uk,
+                              double* Uk, double* wpred, int32_t* exitflag, int32_t* inner_iters, size_t lds,
+                              hipStream_t st);
