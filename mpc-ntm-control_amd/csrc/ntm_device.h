@@ -68,6 +68,8 @@ struct Prob {
     int32_t* stats;   // optional per-scenario counters (4 x B, SoA): QP solves,
                       // GI iterations, final active rows, general (state) active rows
     Gen g;
+    double* far;      // far workspace (HBM, far_doubles(N) per scenario) of the kernels
+                      // whose WS keeps J/R out of LDS (ws_far); null otherwise
 };
 
 constexpr double kInf = __builtin_huge_val();
@@ -391,12 +393,28 @@ __device__ __forceinline__ double coef_b(const Coef& k, double r3) { return k.bc
 // GEN: the kernel is built with the scenario generator (per-scenario plasma in
 // the workspace, plant disturbances); without it those paths are compiled out
 // (they cost the N=20 step kernel 2% through register allocation even when off)
+//
+// FAR (long horizons, ws_far): the J/R block (GI's factors and the bordered KKT
+// factor; 41 KB of the 78.5 KB at N = 50) lives in a per-scenario HBM block
+// (Prob::far, L2/MALL-resident while the wave runs) instead of LDS, and the
+// echelon re-solve's sorted E moves to an LDS block of its own, packed lower
+// triangular (row t at t(t+1)/2).  That takes the N = 50 workspace from 78.5 KB
+// to 47.9 KB: 3 scenarios per CU instead of 2 (one wave on each of 3 SIMDs
+// instead of 2).  The certified re-solve of an echelon set, the common path,
+// stays LDS-only; GI and the bordered elimination read and write HBM.
+#ifndef NTM_FAR_MIN_N
+#define NTM_FAR_MIN_N 33
+#endif
+__host__ __device__ constexpr bool ws_far(int NN) { return NN >= NTM_FAR_MIN_N; }
+
 template <int NN, bool GEN = false>
 struct WS {
     static constexpr int kNN = NN;
     static constexpr bool kGen = GEN;
+    static constexpr bool kFar = ws_far(NN);
     int N_rt;
     double* base;
+    double* far;       // kFar: this scenario's J/R block in HBM
     __device__ __forceinline__ int n() const { return NN > 0 ? NN : N_rt; }
     __device__ __forceinline__ int ldj() const { return n() | 1; }
     __device__ __forceinline__ int ldg() const { return 2 * n(); }
@@ -407,7 +425,11 @@ struct WS {
     // halve the scenarios per CU, and the dual direction falls back to back substitution
     __device__ __forceinline__ bool useT() const { return n() <= kMaxNT; }
     __device__ __forceinline__ int oT() const { return oR() + (n() + 1) * ldj(); }
-    __device__ __forceinline__ int oV() const { return oT() + (useT() ? n() * ldj() : 0); }   // vector block
+    // kFar: the E block (packed lower-triangular E, then 2(N+1) ints) replaces J/R/T in LDS
+    __device__ __forceinline__ int oV() const {
+        if constexpr (kFar) return oJ() + (n() * (n() + 1)) / 2 + (n() + 1);
+        else return oT() + (useT() ? n() * ldj() : 0);   // vector block
+    }
     __device__ __forceinline__ double* rho() const { return base; }                 // 3N (3xN col-major)
     __device__ __forceinline__ double* a11() const { return base + 3 * n(); }         // n()
     __device__ __forceinline__ double* a21() const { return base + 4 * n(); }         // n()
@@ -419,13 +441,36 @@ struct WS {
     __device__ __forceinline__ double* Gt() const { return base + 14 * n(); }         // n()(n()+1)
     __device__ __forceinline__ int gidx(int r, int j) const { return j * (2 * n() - j + 1) + r - 2 * j; }
     __device__ __forceinline__ double& gt(int r, int j) const { return Gt()[gidx(r, j)]; }   // r >= 2j
-    __device__ __forceinline__ double* J() const { return base + oJ(); }            // n() x ldj() row-major
+    __device__ __forceinline__ double* J() const {                                   // n() x ldj() row-major
+        if constexpr (kFar) return far;
+        else return base + oJ();
+    }
     // R: n() rows x (n()+1) columns col-major; the polish keeps its Schur complement
     // K in the strict upper triangle: K(a, c), a >= c, at R[c + (a+1) ldj()]
-    __device__ __forceinline__ double* R() const { return base + oR(); }
+    __device__ __forceinline__ double* R() const {
+        if constexpr (kFar) return far + n() * ldj();
+        else return base + oR();
+    }
     // T = R^{-1} of the GI factorisation (upper triangular, row-major n() x ldj();
     // zero outside the leading q x q block), so the dual direction is a matvec
-    __device__ __forceinline__ double* T() const { return base + oT(); }
+    __device__ __forceinline__ double* T() const {
+        if constexpr (kFar) return far + (2 * n() + 1) * ldj();
+        else return base + oT();
+    }
+    // echelon re-solve: sorted E (entry (t, u), u <= t, at Ep()[eidx(t, u)]) and the
+    // row permutation / column owner ints (2(N+1)); in the J/R block unless kFar
+    __device__ __forceinline__ double* Ep() const {
+        if constexpr (kFar) return base + oJ();
+        else return J();
+    }
+    __device__ __forceinline__ int eidx(int t, int u) const {
+        if constexpr (kFar) return (t * (t + 1)) / 2 + u;
+        else return t * ldj() + u;
+    }
+    __device__ __forceinline__ int* permi() const {
+        if constexpr (kFar) return reinterpret_cast<int*>(base + oJ() + (n() * (n() + 1)) / 2);
+        else return reinterpret_cast<int*>(R());
+    }
     // 2N ints (in 2N doubles of space): per state row r, (last column j with
     // Gamma_rj != 0) + 1, plus kRowMulti if it has two or more non-zeros
     __device__ __forceinline__ int* rinfo() const { return reinterpret_cast<int*>(base + oV()); }
@@ -464,24 +509,32 @@ struct WS {
 };
 
 __host__ __device__ inline int ldj_of(int N) { return N | 1; }
-__host__ __device__ inline int ws_doubles(int N) {
-    return 14 * N + N * (N + 1) + (N <= kMaxNT ? 2 : 1) * N * ldj_of(N) + (N + 1) * ldj_of(N) + 24 * N + 6;
+// the J/R(/T) block: in LDS, or in HBM per scenario (far)
+__host__ __device__ inline int far_doubles(int N) {
+    return (N <= kMaxNT ? 2 : 1) * N * ldj_of(N) + (N + 1) * ldj_of(N);
+}
+__host__ __device__ inline int ws_doubles(int N, bool far = false) {
+    const int jr = far ? (N * (N + 1)) / 2 + (N + 1) : far_doubles(N);
+    return 14 * N + N * (N + 1) + jr + 24 * N + 6;
 }
 // workspace bytes with room for `rows` active-row flags: the structured rows of
 // the MPC step are at most 8N+2 (getWLc 6N+4 plus 2(N-1) rate rows); a dense
 // quadprog problem (k_qp) may carry more
-__host__ __device__ inline int ws_bytes_rows(int N, int rows) {
+__host__ __device__ inline int ws_bytes_rows(int N, int rows, bool far = false) {
     const int flags = rows > 8 * N + 4 ? rows : 8 * N + 4;
-    int b = ws_doubles(N) * 8 + 6 * (N + 1) * 4 + N + flags;   // ..., fx (N), aflag
+    int b = ws_doubles(N, far) * 8 + 6 * (N + 1) * 4 + N + flags;   // ..., fx (N), aflag
     return (b + 15) & ~15;
 }
-__host__ __device__ inline int ws_bytes(int N) { return ws_bytes_rows(N, 8 * N + 4); }
+__host__ __device__ inline int ws_bytes(int N, bool far = false) { return ws_bytes_rows(N, 8 * N + 4, far); }
 
+// s: the scenario's index in the launch (its far block, when the WS has one)
 template <int NN, bool GEN = false>
-__device__ inline WS<NN, GEN> ws_carve(char* base, int N) {
+__device__ inline WS<NN, GEN> ws_carve(char* base, int N, const Prob* pb = nullptr, int64_t s = 0) {
     WS<NN, GEN> w;
     w.N_rt = N;
     w.base = reinterpret_cast<double*>(base);
+    w.far = nullptr;
+    if constexpr (WS<NN, GEN>::kFar) w.far = pb->far + s * (int64_t)far_doubles(N);
     return w;
 }
 
@@ -2062,7 +2115,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     //     by back substitution in the certificate; no Gram of the free columns and
     //     no bordered elimination.  perm[t] = the general row whose last free
     //     variable is the t-th (scratch ints in the R block; E goes to the J block).
-    int* const perm = reinterpret_cast<int*>(w.R());      // sorted row t -> general row
+    int* const perm = w.permi();                           // sorted row t -> general row
     int* const colrow = perm + (N + 1);                    // compact column -> row ending there
     bool sq = false;                                       // echelon path (k = nF - nS <= 1)
     int nc = -1;                                           // k = 1: the non-pivot compact column
@@ -2198,9 +2251,14 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         // the non-pivot column e_c (k = 1) and h
         const int n = nS - (xb >= 0 ? 1 : 0);
         auto pc = [&](int u) { return u + ((nc >= 0 && u >= nc) ? 1 : 0); };
+        double* const Ep = w.Ep();
         for (int idx = l; idx < n * n; idx += P) {
             const int t = idx / n, u = idx - t * n;
-            Lp[t * LD + u] = (u <= t) ? gen_n(perm[t], w.fidx()[pc(u)]) : 0.0;
+            if constexpr (W::kFar) {                               // packed: the lower triangle only
+                if (u <= t) Ep[w.eidx(t, u)] = gen_n(perm[t], w.fidx()[pc(u)]);
+            } else {
+                Ep[w.eidx(t, u)] = (u <= t) ? gen_n(perm[t], w.fidx()[pc(u)]) : 0.0;
+            }
         }
         double acc = 0.0, acz = 0.0;
         if (l < n) {
@@ -2209,15 +2267,15 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         }
         const double hxb = (kCollision && xb >= 0) ? hs_of(xb) : 0.0;   // before w.Phi() is reused
         NTM_WSYNC();
-        if (l < n) sq_id = 1.0 / Lp[l * LD + l];
+        if (l < n) sq_id = 1.0 / Ep[w.eidx(l, l)];
         NTM_ACC(ST_S_E, tp);
         // E_p V_p = h and (k = 1) E_p Z_p = -e_c: lane t owns row t; step t broadcasts
         // x_t (z_t) and updates the rows below
         double x = 0.0, zz = 0.0;
-        double en = (l > 0 && l < n) ? Lp[l * LD] : 0.0;      // E[l][t], loaded one step ahead
+        double en = (l > 0 && l < n) ? Ep[w.eidx(l, 0)] : 0.0;   // E[l][t], loaded one step ahead
         for (int t = 0; t < n; ++t) {
             const double et = en;
-            if (t + 1 < n) en = (l > t + 1 && l < n) ? Lp[l * LD + t + 1] : 0.0;
+            if (t + 1 < n) en = (l > t + 1 && l < n) ? Ep[w.eidx(l, t + 1)] : 0.0;
             const double xt = gbcast<P>(acc * sq_id, t);
             if (l == t) x = xt;
             acc -= et * xt;
@@ -2563,7 +2621,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             // one collision: a second right-hand side, the left-out row B at the pivot columns
             double acb = (kCollision && xb >= 0 && l < n) ? gen_n(xb, w.fidx()[pl]) : 0.0, mb = 0.0;
             for (int u = n - 1; u >= 0; --u) {
-                const double eu = (l < u) ? Lp[u * LD + l] : 0.0;
+                const double eu = (l < u) ? w.Ep()[w.eidx(u, l)] : 0.0;
                 const double mu_u = gbcast<P>(acc * sq_id, u);
                 if (l == u) mu = mu_u;
                 acc -= eu * mu_u;

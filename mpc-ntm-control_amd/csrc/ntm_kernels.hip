@@ -395,6 +395,8 @@ struct ntm_ctx {
     std::string err;
     void* dbuf = nullptr;
     size_t dbuf_bytes = 0;
+    void* fbuf = nullptr;       // far workspaces of the long-horizon kernels (ws_far)
+    size_t fbuf_bytes = 0;
     hipStream_t stream = nullptr;
 };
 
@@ -456,12 +458,35 @@ int set_lds(ntm_ctx* ctx, K kern, size_t lds) {
     return NTM_OK;
 }
 
+// the far workspace (J/R in HBM, far_doubles(N) per scenario) of a kernel whose WS
+// keeps it out of LDS; grown on demand, one per context (one call at a time)
+template <int NN>
+int attach_far(ntm_ctx* ctx, Prob& pb, int64_t B) {
+    if constexpr (!ws_far(NN)) {
+        return NTM_OK;
+    } else {
+        const size_t bytes = (size_t)B * far_doubles(pb.N) * sizeof(double);
+        if (ctx->fbuf_bytes < bytes) {
+            if (ctx->fbuf) (void)hipFree(ctx->fbuf);
+            ctx->fbuf = nullptr;
+            ctx->fbuf_bytes = 0;
+            int rc = check_hip(ctx, hipMalloc(&ctx->fbuf, bytes), "hipMalloc (far workspace)");
+            if (rc) return fail(ctx, NTM_E_NOMEM, ctx->err);
+            ctx->fbuf_bytes = bytes;
+        }
+        pb.far = static_cast<double*>(ctx->fbuf);
+        return NTM_OK;
+    }
+}
+
+
 template <int P, int NN>
-int launch_step(ntm_ctx* ctx, const Prob& pb, int64_t B, const double* x_k, double* rho, double* U_old,
+int launch_step(ntm_ctx* ctx, Prob pb, int64_t B, const double* x_k, double* rho, double* U_old,
                 double* U, double* x_pred, double* x_next, int32_t* exitflag, int32_t* inner_iters,
                 int32_t* active_ws, hipStream_t st) {
     constexpr int G = 64 / P;
-    size_t lds = (size_t)G * ws_bytes(pb.N);
+    size_t lds = (size_t)G * ws_bytes(pb.N, ws_far(NN));
+    if (int rc = attach_far<NN>(ctx, pb, B)) return rc;
 #ifdef NTM_LDS_PAD
     lds += NTM_LDS_PAD;   // occupancy study only (tools/occupancy_study.sh): fewer scenarios per CU
 #endif
@@ -490,10 +515,11 @@ int launch_step(ntm_ctx* ctx, const Prob& pb, int64_t B, const double* x_k, doub
 }
 
 template <int P, int NN>
-int launch_run(ntm_ctx* ctx, const Prob& pb, int64_t B, int k_sim, const double* x0, double* xk, double* uk,
+int launch_run(ntm_ctx* ctx, Prob pb, int64_t B, int k_sim, const double* x0, double* xk, double* uk,
                double* Uk, double* wpred, int32_t* exitflag, int32_t* inner_iters, hipStream_t st) {
     constexpr int G = 64 / P;
-    size_t lds = (size_t)G * ws_bytes(pb.N);
+    size_t lds = (size_t)G * ws_bytes(pb.N, ws_far(NN));
+    if (int rc = attach_far<NN>(ctx, pb, B)) return rc;
 #ifndef NTM_SINGLE_TU
     if constexpr (NN == 50) {                          // ntm_n50.hip
         if (lds > 160 * 1024) return fail(ctx, NTM_E_UNSUPPORTED, "LDS workspace exceeds 160 KiB");
@@ -630,6 +656,7 @@ int ntm_ctx_create(ntm_ctx** out, int32_t device) {
 void ntm_ctx_destroy(ntm_ctx* ctx) {
     if (!ctx) return;
     DeviceGuard dg(ctx);
+    if (ctx->fbuf) (void)hipFree(ctx->fbuf);
     if (ctx->dbuf) (void)hipFree(ctx->dbuf);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

@@ -157,12 +157,12 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, 
     NTM_STAMPS_INIT();
     NTM_TRACE_SET(s, g, l);
     if (s >= B) return;
-    auto w = ws_carve<NN, GEN>(smem + g * ws_bytes(N), N);
+    auto w = ws_carve<NN, GEN>(smem + g * ws_bytes(N, ws_far(NN)), N, &pb, s);
 #ifdef NTM_POISON
     // debug build (make poison): the workspace starts as NTM_POISON-valued doubles, so
     // a read of LDS this launch never wrote shows up as a run-to-run difference
     // (tools/determinism.py + compare_runs.py; this found the x_0-row read of rinfo[-1])
-    for (int e = l; e < ws_bytes(N) / 8; e += P) w.base[e] = NTM_POISON;
+    for (int e = l; e < ws_bytes(N, ws_far(NN)) / 8; e += P) w.base[e] = NTM_POISON;
     NTM_WSYNC();
 #endif
     const double x0 = x_k[2 * s], x1 = x_k[2 * s + 1];
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_run(Prob pb, i
     const int64_t s = xcd_swizzle(blockIdx.x, gridDim.x) * G + g;
     const int N = NN > 0 ? NN : pb.N;
     if (s >= B) return;
-    auto w = ws_carve<NN, true>(smem + g * ws_bytes(N), N);
+    auto w = ws_carve<NN, true>(smem + g * ws_bytes(N, ws_far(NN)), N, &pb, s);
     double x0 = x0v[2 * s], x1 = x0v[2 * s + 1];
     if (l < 2) w.cand()[l * (N + 1) + N] = -1;
     scn_store(pb, w, pb.g.first_id + s, l);           // this scenario's plasma (generator)
