@@ -394,18 +394,26 @@ __device__ __forceinline__ double coef_b(const Coef& k, double r3) { return k.bc
 // the workspace, plant disturbances); without it those paths are compiled out
 // (they cost the N=20 step kernel 2% through register allocation even when off)
 //
-// FAR (long horizons, ws_far): the J/R block (GI's factors and the bordered KKT
-// factor; 41 KB of the 78.5 KB at N = 50) lives in a per-scenario HBM block
-// (Prob::far, L2/MALL-resident while the wave runs) instead of LDS, and the
-// echelon re-solve's sorted E moves to an LDS block of its own, packed lower
-// triangular (row t at t(t+1)/2).  That takes the N = 50 workspace from 78.5 KB
-// to 47.9 KB: 3 scenarios per CU instead of 2 (one wave on each of 3 SIMDs
-// instead of 2).  The certified re-solve of an echelon set, the common path,
-// stays LDS-only; GI and the bordered elimination read and write HBM.
-#ifndef NTM_FAR_MIN_N
-#define NTM_FAR_MIN_N 33
+// FAR (ws_far: N = 20 and N > 32): the J/R(/T) block (GI's factors and the
+// bordered KKT factor) lives in a per-scenario HBM block (Prob::far, L2-resident
+// while the wave runs) instead of LDS, and the echelon re-solve's sorted E moves
+// to an LDS block of its own, packed lower triangular (row t at t(t+1)/2).  The
+// certified re-solve of an echelon set, the common path, stays LDS-only; GI and
+// the bordered elimination read and write HBM.  More scenarios fit a CU:
+//   N = 50: 78.5 -> 47.9 KB, 3 scenarios per CU instead of 2 (one wave on each
+//           of 3 SIMDs instead of 2; the kernel has the 512-register budget of
+//           one wave per SIMD either way);
+//   N = 20: 20.4 -> 12.0 KB, 12 scenarios per CU instead of 8, i.e. 3 waves per
+//           SIMD, which the kernel is built for (168 VGPRs, NTM_WAVES_PER_EU).
+// Neither pays without the occupancy: at 2 waves per SIMD the N = 20 kernel is 6%
+// slower with its GI in HBM.  NTM_FAR_N20=0 builds the all-LDS N = 20 kernel.
+#ifndef NTM_FAR_N20
+#define NTM_FAR_N20 1
 #endif
-__host__ __device__ constexpr bool ws_far(int NN) { return NN >= NTM_FAR_MIN_N; }
+#ifndef NTM_FAR_COLMAJOR
+#define NTM_FAR_COLMAJOR 0   // 1: J, T and the bordered factor column-major in the far block (slower)
+#endif
+__host__ __device__ constexpr bool ws_far(int NN) { return NN > 32 || (NTM_FAR_N20 && NN == 20); }
 
 template <int NN, bool GEN = false>
 struct WS {
@@ -456,6 +464,20 @@ struct WS {
     __device__ __forceinline__ double* T() const {
         if constexpr (kFar) return far + (2 * n() + 1) * ldj();
         else return base + oT();
+    }
+    // element (r, c) of J (and of T) at J()[r jr() + c jc()]: row-major in LDS,
+    // column-major in HBM (kFar), where the common access, each lane walking its own
+    // row, is then one coalesced load per column instead of 64 cache lines
+    static constexpr bool kCol = kFar && NTM_FAR_COLMAJOR;
+    __device__ __forceinline__ int jr() const { return kCol ? 1 : ldj(); }
+    __device__ __forceinline__ int jc() const { return kCol ? ldj() : 1; }
+    // packed bordered KKT factor (rows 0..nt, row nt the right-hand side), entry
+    // (r, c), c <= r, at J()[brow(r) + bcol(c, nt)]: row-major (row r at r(r+1)/2) in
+    // LDS, column-major (column c at c(nt+1) - c(c-1)/2) in HBM, where a lane owns a
+    // row and the elimination walks the columns
+    __device__ __forceinline__ int brow(int r) const { return kCol ? r : (r * (r + 1)) / 2; }
+    __device__ __forceinline__ int bcol(int c, int nt) const {
+        return kCol ? c * (nt + 1) - (c * (c - 1)) / 2 - c : c;
     }
     // echelon re-solve: sorted E (entry (t, u), u <= t, at Ep()[eidx(t, u)]) and the
     // row permutation / column owner ints (2(N+1)); in the J/R block unless kFar
@@ -664,7 +686,7 @@ __device__ __forceinline__ double sub_dot(double s, const double* a, int sa, con
 }
 // a[j] -= f b[j] for lo <= j < hi, the loads of CH entries issued ahead of their stores
 template <int CH>
-__device__ __forceinline__ void axpy_sub(double* a, const double* b, double f, int lo, int hi) {
+__device__ __forceinline__ void axpy_sub(double* a, const double* b, double f, int lo, int hi, int sa = 1) {
     NTM_CHUNK_PRAGMA
     for (int j0 = lo; j0 < hi; j0 += CH) {
         double x[CH], z[CH];
@@ -672,13 +694,13 @@ __device__ __forceinline__ void axpy_sub(double* a, const double* b, double f, i
         for (int u = 0; u < CH; ++u) {
             const int j = j0 + u;
             const bool in = j < hi;
-            x[u] = in ? a[j] : 0.0;
+            x[u] = in ? a[j * sa] : 0.0;
             z[u] = in ? b[j] : 0.0;
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < CH; ++u)
-            if (j0 + u < hi) a[j0 + u] = x[u] - f * z[u];
+            if (j0 + u < hi) a[(j0 + u) * sa] = x[u] - f * z[u];
     }
 }
 // Gamma_r v restricted to j <= r/2 (row r of the packed block-lower-triangular Gamma)
@@ -1463,7 +1485,8 @@ __device__ __forceinline__ double bwd_lanes(const double* L, const double* rdiag
 template <int P, class Rows, class W>
 __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, int l, int* iters_out, int* q_out,
                         int nwarm = 0) {
-    const int N = w.n(), LD = w.ldj(), LDJ = w.ldj();
+    const int N = w.n(), LD = w.ldj();
+    const int JR = w.jr(), JC = w.jc();     // J(r, c) at r JR + c JC (T alike)
     *iters_out = 0;
     *q_out = 0;
     NTM_T0(tg);
@@ -1474,10 +1497,10 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
         for (int i = 0; i < N; ++i) {
             double x = 0.0;
             if (i >= l) {
-                x = sub_dot<NTM_CH>((i == l) ? 1.0 : 0.0, w.R() + i, LD, w.J() + l * LDJ, 1, l, i);
+                x = sub_dot<NTM_CH>((i == l) ? 1.0 : 0.0, w.R() + i, LD, w.J() + l * JR, JC, l, i);
                 x *= w.ldi()[i];
             }
-            w.J()[l * LDJ + i] = x;
+            w.J()[l * JR + i * JC] = x;
         }
     }
     NTM_WSYNC();
@@ -1485,11 +1508,11 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
     double Vl = 0.0;
     {
         double t = 0.0;
-        if (l < N) t = dot_batched<NTM_CH>(w.J() + l, LDJ, w.F(), 1, N);
+        if (l < N) t = dot_batched<NTM_CH>(w.J() + l * JC, JR, w.F(), 1, N);
         if (l < N) w.d()[l] = t;
         NTM_WSYNC();
         if (l < N) {
-            const double v = dot_batched<NTM_CH>(w.J() + l * LDJ, 1, w.d(), 1, N);
+            const double v = dot_batched<NTM_CH>(w.J() + l * JR, JC, w.d(), 1, N);
             Vl = -v;
             w.V()[l] = Vl;
             w.U()[l] = w.D()[l] * Vl;
@@ -1499,7 +1522,7 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
     NTM_ACC(ST_GI_FACT, tg);
     if (!has_rows) return NTM_EXIT_OPTIMAL;
     const bool useT = w.useT();
-    if (useT && l < N) for (int b = 0; b < N; ++b) w.T()[l * LDJ + b] = 0.0;
+    if (useT && l < N) for (int b = 0; b < N; ++b) w.T()[l * JR + b * JC] = 0.0;
     const int max_iter = 10 * (N + nrows) + 50;
     int q = 0, it = 0;
     // Warm start: the rows w.sidx()[0..nwarm) of a failed
@@ -1526,15 +1549,15 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
             }
             if (ej >= 0) {                        // u-bound row: n_p = -+e_j, d = J' n_p a signed row of J
                 bcp = uni<P>(-(rows.bval(w, p) / rows.rnorm(w, p)));
-                if (l < N) dl = esg * w.J()[ej * LDJ + l];
+                if (l < N) dl = esg * w.J()[ej * JR + l * JC];
             } else {
                 bcp = uni<P>(rows.template load_np<P>(w, p, l));
-                if (l < N) dl = dot_batched<NTM_CH>(w.J() + l, LDJ, w.np(), 1, N);
+                if (l < N) dl = dot_batched<NTM_CH>(w.J() + l * JC, JR, w.np(), 1, N);
             }
             if (l < N) { w.d()[l] = (l >= q) ? dl : 0.0; w.dr()[l] = (l < q) ? dl : 0.0; }
             NTM_WSYNC();
             double rl = 0.0;
-            if (useT && l < N) rl = dot_batched<NTM_CH>(w.T() + l * LDJ, 1, w.dr(), 1, N);
+            if (useT && l < N) rl = dot_batched<NTM_CH>(w.T() + l * JR, JC, w.dr(), 1, N);
             const double zn = gsum<P>((l >= q && l < N) ? dl * dl : 0.0);
             const double dnrm = gsum<P>(dl * dl);
             if (q >= N) { NTM_CNT(CN_WARM_FULL); break; }
@@ -1553,19 +1576,19 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
                 double vtv = gsum<P>(vl * vl);
                 NTM_WSYNC();
                 if (l < N) {
-                    const double dot = dot_batched<NTM_CH>(w.J() + l * LDJ, 1, w.hv(), 1, N);
+                    const double dot = dot_batched<NTM_CH>(w.J() + l * JR, JC, w.hv(), 1, N);
                     const double f = 2.0 * dot / vtv;
-                    axpy_sub<NTM_CH>(w.J() + l * LDJ, w.hv(), f, q, N);
+                    axpy_sub<NTM_CH>(w.J() + l * JR, w.hv(), f, q, N, JC);
                 }
             }
             const double ih = 1.0 / h;
             if (l < q) {
                 w.R()[l + q * LD] = dl;
-                if (useT) w.T()[l * LDJ + q] = -rl * ih;
+                if (useT) w.T()[l * JR + q * JC] = -rl * ih;
             }
             if (l == q) {
                 w.R()[q + q * LD] = h;
-                if (useT) w.T()[q * LDJ + q] = ih;
+                if (useT) w.T()[q * JR + q * JC] = ih;
                 w.act()[q] = p;
                 w.aflag()[p] = kActiveRow;
                 w.Vb()[q] = bcp;                     // bc of active row q (scratch)
@@ -1576,9 +1599,9 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
         if (okw) {
             // c = J' F~ (lane k), wv = (T' bc)_k for k < q
             double c = 0.0, wv = 0.0;
-            if (l < N) c = dot_batched<NTM_CH>(w.J() + l, LDJ, w.F(), 1, N);
+            if (l < N) c = dot_batched<NTM_CH>(w.J() + l * JC, JR, w.F(), 1, N);
             if (useT) {
-                if (l < q) wv = dot_range<NTM_CH>(w.T() + l, LDJ, w.Vb(), 1, 0, l + 1);
+                if (l < q) wv = dot_range<NTM_CH>(w.T() + l * JC, JR, w.Vb(), 1, 0, l + 1);
             } else {                                 // long horizons: R' wv = bc by forward substitution
                 double acc = (l < q) ? w.Vb()[l] : 0.0;
                 for (int k2 = 0; k2 < q; ++k2) {
@@ -1594,9 +1617,9 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
             }
             NTM_WSYNC();
             double v = 0.0, u = 0.0;
-            if (l < N) for (int k2 = 0; k2 < N; ++k2) v += w.J()[l * LDJ + k2] * (w.dr()[k2] - w.d()[k2]);
+            if (l < N) for (int k2 = 0; k2 < N; ++k2) v += w.J()[l * JR + k2 * JC] * (w.dr()[k2] - w.d()[k2]);
             if (useT) {
-                if (l < q) u = dot_range<NTM_CH>(w.T() + l * LDJ, 1, w.np(), 1, l, q);
+                if (l < q) u = dot_range<NTM_CH>(w.T() + l * JR, JC, w.np(), 1, l, q);
             } else {                                 // R u = wv + c1 by back substitution
                 double acc = (l < q) ? w.np()[l] : 0.0;
                 for (int b = q - 1; b >= 0; --b) {
@@ -1660,9 +1683,9 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
             // d = J' n_p
             double dl = 0.0;
             if (ej >= 0) {
-                if (l < N) dl = esg * w.J()[ej * LDJ + l];
+                if (l < N) dl = esg * w.J()[ej * JR + l * JC];
             } else if (l < N) {
-                dl = dot_batched<NTM_CH>(w.J() + l, LDJ, w.np(), 1, N);
+                dl = dot_batched<NTM_CH>(w.J() + l * JC, JR, w.np(), 1, N);
             }
             // d split at q: d2 = d[q:N] (w.d) and d1 = d[0:q] (w.dr), zero elsewhere, so
             // both matvecs run full fixed-length rows (unrolled, loads batched)
@@ -1671,8 +1694,8 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
             // z = J2 d2 (primal direction) and r = T d1 = R^{-1} d1 (negative dual direction)
             double zl = 0.0, rl = 0.0;
             if (l < N) {
-                zl = dot_batched<NTM_CH>(w.J() + l * LDJ, 1, w.d(), 1, N);
-                if (useT) rl = dot_batched<NTM_CH>(w.T() + l * LDJ, 1, w.dr(), 1, N);
+                zl = dot_batched<NTM_CH>(w.J() + l * JR, JC, w.d(), 1, N);
+                if (useT) rl = dot_batched<NTM_CH>(w.T() + l * JR, JC, w.dr(), 1, N);
             }
             if (!useT) {                       // long horizons: back substitution on R
                 double acc = (l < q) ? dl : 0.0;
@@ -1717,20 +1740,20 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
                         double vtv = gsum<P>(vl * vl);
                         NTM_WSYNC();
                         if (l < N) {
-                            const double dot = dot_batched<NTM_CH>(w.J() + l * LDJ, 1, w.hv(), 1, N);
+                            const double dot = dot_batched<NTM_CH>(w.J() + l * JR, JC, w.hv(), 1, N);
                             const double f = 2.0 * dot / vtv;
-                            axpy_sub<NTM_CH>(w.J() + l * LDJ, w.hv(), f, q, N);
+                            axpy_sub<NTM_CH>(w.J() + l * JR, w.hv(), f, q, N, JC);
                         }
                     }
                     // R gains column q = [d1; h]; T = R^{-1} gains column q = [-r/h; 1/h]
                     const double ih = 1.0 / h;
                     if (l < q) {
                         w.R()[l + q * LD] = dl;
-                        if (useT) w.T()[l * LDJ + q] = -rl * ih;
+                        if (useT) w.T()[l * JR + q * JC] = -rl * ih;
                     }
                     if (l == q) {
                         w.R()[q + q * LD] = h;
-                        if (useT) w.T()[q * LDJ + q] = ih;
+                        if (useT) w.T()[q * JR + q * JC] = ih;
                         w.act()[q] = p;
                         w.aflag()[p] = kActiveRow;
                         w.uu()[q] = upq;
@@ -1771,24 +1794,24 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
                     w.R()[(j + 1) + l * LD] = (l == j) ? 0.0 : (-ss * r1 + cc * r2);
                 }
                 if (l < N) {
-                    double j1 = w.J()[l * LDJ + j], j2 = w.J()[l * LDJ + j + 1];
-                    w.J()[l * LDJ + j] = cc * j1 + ss * j2;
-                    w.J()[l * LDJ + j + 1] = -ss * j1 + cc * j2;
+                    double j1 = w.J()[l * JR + j * JC], j2 = w.J()[l * JR + (j + 1) * JC];
+                    w.J()[l * JR + j * JC] = cc * j1 + ss * j2;
+                    w.J()[l * JR + (j + 1) * JC] = -ss * j1 + cc * j2;
                 }
                 if (useT && l < q) {   // T <- T G_j' (the columns rotate like J's)
-                    double t1v = w.T()[l * LDJ + j], t2v = w.T()[l * LDJ + j + 1];
-                    w.T()[l * LDJ + j] = cc * t1v + ss * t2v;
-                    w.T()[l * LDJ + j + 1] = -ss * t1v + cc * t2v;
+                    double t1v = w.T()[l * JR + j * JC], t2v = w.T()[l * JR + (j + 1) * JC];
+                    w.T()[l * JR + j * JC] = cc * t1v + ss * t2v;
+                    w.T()[l * JR + (j + 1) * JC] = -ss * t1v + cc * t2v;
                 }
                 NTM_WSYNC();
             }
             // R'^{-1} = (T Q) without row l0 and column q-1.  Lane c owns column c:
             // rows l0+1..q-1 move up one; the discarded column q-1 is cleared
             if (useT && l < q - 1) {
-                for (int a = l0; a < q - 1; ++a) w.T()[a * LDJ + l] = w.T()[(a + 1) * LDJ + l];
-                w.T()[(q - 1) * LDJ + l] = 0.0;
+                for (int a = l0; a < q - 1; ++a) w.T()[a * JR + l * JC] = w.T()[(a + 1) * JR + l * JC];
+                w.T()[(q - 1) * JR + l * JC] = 0.0;
             } else if (useT && l == q - 1) {
-                for (int a = 0; a < q; ++a) w.T()[a * LDJ + l] = 0.0;
+                for (int a = 0; a < q; ++a) w.T()[a * JR + l * JC] = 0.0;
             }
             NTM_WSYNC();
             --q;
@@ -2188,7 +2211,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         NNc > 0 && (2 * NNc) * (2 * NNc + 1) / 2 + 2 * NNc <= NNc * LDc + (NNc + 1) * LDc;
     const bool fused = kAlwaysFused || ((nt + 1 <= RPL * P) && (nt * (nt + 1) / 2 + nt <= N * LDJ + (N + 1) * LD));
     double* const Lp = w.J();
-    if (!sq && fused && l < nF) Lp[(nt * (nt + 1)) / 2 + l] = -gl;
+    if (!sq && fused && l < nF) Lp[w.brow(nt) + w.bcol(l, nt)] = -gl;
     // --- compact G~_FF: one (a, c) entry per lane (packed rows, or lower col-major in R) ---
     {
         const int npair = sq ? 0 : nF * (nF + 1) / 2;
@@ -2202,7 +2225,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             const double* cc = w.Gt() + w.gidx(2 * jc, jc) - 2 * jc;
             const double sg = qdot_rows<NTM_CH>(ca, cc, N, ja, q00, q01, q10, q11);   // terms i < ja masked
             const double gv = (2 * sg) * w.D()[ja] * w.D()[jc];
-            if (fused) Lp[idx] = gv;                                  // idx == a(a+1)/2 + c
+            if (fused) Lp[w.brow(a) + w.bcol(c, nt)] = gv;            // row-major: idx == a(a+1)/2 + c
             else w.R()[a + c * LD] = gv;
         }
     }
@@ -2340,9 +2363,9 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         // block of A is zero and is never stored (the elimination starts it at 0)
         for (int idx = l; idx < nF * nS; idx += P) {
             const int s2 = idx / nF, a = idx - s2 * nF;
-            Lp[((nF + s2) * (nF + s2 + 1)) / 2 + a] = gen_n(s2, w.fidx()[a]);
+            Lp[w.brow(nF + s2) + w.bcol(a, nt)] = gen_n(s2, w.fidx()[a]);
         }
-        if (l < nS) Lp[(nt * (nt + 1)) / 2 + nF + l] = hs_of(l);
+        if (l < nS) Lp[w.brow(nt) + w.bcol(nF + l, nt)] = hs_of(l);
         NTM_WSYNC();
         NTM_ACC(ST_S_E, tp);
         // Left-looking elimination of A = [[G~_FF, E'], [E, 0]] = L_A diag(I, -I) L_A'
@@ -2362,7 +2385,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
 #pragma unroll
         for (int r = 0; r < RPL; ++r) {
             const int lr = l + r * P;
-            myrow[r] = Lp + (lr * (lr + 1)) / 2;
+            myrow[r] = Lp + w.brow(lr);
         }
         if (ok) {
             // blocks of KB columns: one pass of loads over the finished columns j < k
@@ -2381,7 +2404,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
 #pragma unroll
                     for (int b2 = 0; b2 < KB; ++b2) {
                         const int col = k + b2;
-                        sacc[r][b2] = (b2 < kb && live[r] && lr >= col) ? ((col >= nF && lr < nt) ? 0.0 : myrow[r][col])
+                        sacc[r][b2] = (b2 < kb && live[r] && lr >= col) ? ((col >= nF && lr < nt) ? 0.0 : myrow[r][w.bcol(col, nt)])
                                                                         : 0.0;
                     }
                 }
@@ -2392,19 +2415,20 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
 #pragma unroll
                 for (int b2 = 0; b2 < KB; ++b2) {
                     const int rr = (k + b2 < nt) ? k + b2 : nt;
-                    prb[b2] = Lp + (rr * (rr + 1)) / 2;
+                    prb[b2] = Lp + w.brow(rr);
                 }
 #pragma unroll
                 for (int r = 0; r < RPL; ++r) {
                     if (!live[r]) continue;
                     for (int j = 0; j < k; j += 2) {
                         const bool in1 = j + 1 < k;
-                        const double a0 = myrow[r][j], a1 = myrow[r][j + 1];
+                        const int cj0 = w.bcol(j, nt), cj1 = w.bcol(j + 1, nt);
+                        const double a0 = myrow[r][cj0], a1 = myrow[r][cj1];
                         double p0[KB], p1[KB];
 #pragma unroll
                         for (int b2 = 0; b2 < KB; ++b2) {
-                            p0[b2] = prb[b2][j];
-                            p1[b2] = prb[b2][j + 1];
+                            p0[b2] = prb[b2][cj0];
+                            p1[b2] = prb[b2][cj1];
                         }
                         const double s0 = (j < kf) ? -1.0 : 1.0, s1 = (j + 1 < kf) ? -1.0 : 1.0;
 #pragma unroll
@@ -2453,7 +2477,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                     const int lr = l + r * P;
 #pragma unroll
                     for (int b2 = 0; b2 < KB; ++b2)
-                        if (b2 < kb && lr >= k + b2 && lr <= nt) myrow[r][k + b2] = Lc[r][b2];
+                        if (b2 < kb && lr >= k + b2 && lr <= nt) myrow[r][w.bcol(k + b2, nt)] = Lc[r][b2];
                 }
                 NTM_WSYNC();
             }
@@ -2467,7 +2491,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
 #pragma unroll
             for (int r = 0; r < RPL; ++r) {
                 const int lr = l + r * P;
-                acc[r] = (lr < nt) ? Lp[(nt * (nt + 1)) / 2 + lr] : 0.0;
+                acc[r] = (lr < nt) ? Lp[w.brow(nt) + w.bcol(lr, nt)] : 0.0;
                 x[r] = 0.0;
             }
             // the loads of column k-1 are issued before the broadcast of x_k (one-deep pipeline)
@@ -2475,7 +2499,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
 #pragma unroll
             for (int r = 0; r < RPL; ++r) {
                 const int lr = l + r * P;
-                lkn[r] = (nt > 0 && lr < nt - 1) ? Lp[((nt - 1) * nt) / 2 + lr] : 0.0;
+                lkn[r] = (nt > 0 && lr < nt - 1) ? Lp[w.brow(nt - 1) + w.bcol(lr, nt)] : 0.0;
             }
             if (nt > 0) dkn = w.ldi()[nt - 1];
             for (int k = nt - 1; k >= 0; --k) {
@@ -2487,7 +2511,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
 #pragma unroll
                     for (int r = 0; r < RPL; ++r) {
                         const int lr = l + r * P;
-                        lkn[r] = (lr < k - 1) ? Lp[((k - 1) * k) / 2 + lr] : 0.0;
+                        lkn[r] = (lr < k - 1) ? Lp[w.brow(k - 1) + w.bcol(lr, nt)] : 0.0;
                     }
                     dkn = w.ldi()[k - 1];
                 }

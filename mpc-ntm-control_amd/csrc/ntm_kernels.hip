@@ -397,6 +397,7 @@ struct ntm_ctx {
     size_t dbuf_bytes = 0;
     void* fbuf = nullptr;       // far workspaces of the long-horizon kernels (ws_far)
     size_t fbuf_bytes = 0;
+    hipEvent_t fbuf_done = nullptr;   // recorded after the last launch that used fbuf
     hipStream_t stream = nullptr;
 };
 
@@ -459,24 +460,40 @@ int set_lds(ntm_ctx* ctx, K kern, size_t lds) {
 }
 
 // the far workspace (J/R in HBM, far_doubles(N) per scenario) of a kernel whose WS
-// keeps it out of LDS; grown on demand, one per context (one call at a time)
+// keeps it out of LDS; grown on demand, one per context.  Calls return before
+// their kernels finish and may come on different streams (a caller's stream, the
+// context's own for host buffers), so the block is stream-ordered: a launch that
+// uses it waits for the previous one (fbuf_done, recorded by far_release)
 template <int NN>
-int attach_far(ntm_ctx* ctx, Prob& pb, int64_t B) {
+int attach_far(ntm_ctx* ctx, Prob& pb, int64_t B, hipStream_t st) {
     if constexpr (!ws_far(NN)) {
         return NTM_OK;
     } else {
         const size_t bytes = (size_t)B * far_doubles(pb.N) * sizeof(double);
+        int rc;
+        if (!ctx->fbuf_done &&
+            (rc = check_hip(ctx, hipEventCreateWithFlags(&ctx->fbuf_done, hipEventDisableTiming), "hipEventCreate")))
+            return rc;
         if (ctx->fbuf_bytes < bytes) {
+            // hipFree waits for the device, so no launch still reads the old block
             if (ctx->fbuf) (void)hipFree(ctx->fbuf);
             ctx->fbuf = nullptr;
             ctx->fbuf_bytes = 0;
-            int rc = check_hip(ctx, hipMalloc(&ctx->fbuf, bytes), "hipMalloc (far workspace)");
+            rc = check_hip(ctx, hipMalloc(&ctx->fbuf, bytes), "hipMalloc (far workspace)");
             if (rc) return fail(ctx, NTM_E_NOMEM, ctx->err);
             ctx->fbuf_bytes = bytes;
         }
+        if ((rc = check_hip(ctx, hipStreamWaitEvent(st, ctx->fbuf_done, 0), "hipStreamWaitEvent"))) return rc;
         pb.far = static_cast<double*>(ctx->fbuf);
         return NTM_OK;
     }
+}
+template <int NN>
+int far_release(ntm_ctx* ctx, int rc, hipStream_t st) {
+    if constexpr (ws_far(NN)) {
+        if (rc == NTM_OK) rc = check_hip(ctx, hipEventRecord(ctx->fbuf_done, st), "hipEventRecord");
+    }
+    return rc;
 }
 
 
@@ -486,16 +503,18 @@ int launch_step(ntm_ctx* ctx, Prob pb, int64_t B, const double* x_k, double* rho
                 int32_t* active_ws, hipStream_t st) {
     constexpr int G = 64 / P;
     size_t lds = (size_t)G * ws_bytes(pb.N, ws_far(NN));
-    if (int rc = attach_far<NN>(ctx, pb, B)) return rc;
+    if (int rc = attach_far<NN>(ctx, pb, B, st)) return rc;
 #ifdef NTM_LDS_PAD
     lds += NTM_LDS_PAD;   // occupancy study only (tools/occupancy_study.sh): fewer scenarios per CU
 #endif
 #ifndef NTM_SINGLE_TU
-    if constexpr (NN == 50) {                          // ntm_n50.hip
+    if constexpr (P == 64 && (NN == 20 || NN == 50)) {   // ntm_n20.hip, ntm_n50.hip
         if (lds > 160 * 1024) return fail(ctx, NTM_E_UNSUPPORTED, "LDS workspace exceeds 160 KiB");
-        return check_hip(ctx, ntm_launch_step_n50(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters,
-                                                  active_ws, lds, st),
-                         "k_mpc_step<64,50> launch");
+        const hipError_t e = NN == 20 ? ntm_launch_step_n20(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag,
+                                                            inner_iters, active_ws, lds, st)
+                                      : ntm_launch_step_n50(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag,
+                                                            inner_iters, active_ws, lds, st);
+        return far_release<NN>(ctx, check_hip(ctx, e, "k_mpc_step<64,NN> launch"), st);
     } else
 #endif
     {
@@ -510,7 +529,7 @@ int launch_step(ntm_ctx* ctx, Prob pb, int64_t B, const double* x_k, double* rho
     else
         hipLaunchKernelGGL((k_mpc_step<P, NN, false>), dim3((unsigned)blocks), dim3(64), lds, st, pb, B, x_k, rho,
                            U_old, U, x_pred, x_next, exitflag, inner_iters, active_ws);
-    return check_hip(ctx, hipGetLastError(), "k_mpc_step launch");
+    return far_release<NN>(ctx, check_hip(ctx, hipGetLastError(), "k_mpc_step launch"), st);
     }
 }
 
@@ -519,12 +538,14 @@ int launch_run(ntm_ctx* ctx, Prob pb, int64_t B, int k_sim, const double* x0, do
                double* Uk, double* wpred, int32_t* exitflag, int32_t* inner_iters, hipStream_t st) {
     constexpr int G = 64 / P;
     size_t lds = (size_t)G * ws_bytes(pb.N, ws_far(NN));
-    if (int rc = attach_far<NN>(ctx, pb, B)) return rc;
+    if (int rc = attach_far<NN>(ctx, pb, B, st)) return rc;
 #ifndef NTM_SINGLE_TU
-    if constexpr (NN == 50) {                          // ntm_n50.hip
+    if constexpr (P == 64 && (NN == 20 || NN == 50)) {   // ntm_n20.hip, ntm_n50.hip
         if (lds > 160 * 1024) return fail(ctx, NTM_E_UNSUPPORTED, "LDS workspace exceeds 160 KiB");
-        return check_hip(ctx, ntm_launch_run_n50(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st),
-                         "k_mpc_run<64,50> launch");
+        const hipError_t e =
+            NN == 20 ? ntm_launch_run_n20(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st)
+                     : ntm_launch_run_n50(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st);
+        return far_release<NN>(ctx, check_hip(ctx, e, "k_mpc_run<64,NN> launch"), st);
     } else
 #endif
     {
@@ -534,7 +555,7 @@ int launch_run(ntm_ctx* ctx, Prob pb, int64_t B, int k_sim, const double* x0, do
     if (blocks == 0) return NTM_OK;
     hipLaunchKernelGGL((k_mpc_run<P, NN>), dim3((unsigned)blocks), dim3(64), lds, st, pb, B, k_sim, x0, xk, uk, Uk,
                        wpred, exitflag, inner_iters);
-    return check_hip(ctx, hipGetLastError(), "k_mpc_run launch");
+    return far_release<NN>(ctx, check_hip(ctx, hipGetLastError(), "k_mpc_run launch"), st);
     }
 }
 
@@ -657,6 +678,7 @@ void ntm_ctx_destroy(ntm_ctx* ctx) {
     if (!ctx) return;
     DeviceGuard dg(ctx);
     if (ctx->fbuf) (void)hipFree(ctx->fbuf);
+    if (ctx->fbuf_done) (void)hipEventDestroy(ctx->fbuf_done);
     if (ctx->dbuf) (void)hipFree(ctx->dbuf);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;

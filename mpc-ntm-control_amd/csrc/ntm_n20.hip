@@ -1,0 +1,25 @@
+// ntm_n20.hip — the N = 20 specialisation of the hot-path kernels (BASELINE
+// configs 2-4, the headline) in a translation unit of its own, for its own LDS
+// batch size.  With the far workspace and 3 waves per SIMD (168 VGPRs), measured
+// on the MI355X (B = 1e5, ms per step-batch over steps 6-25, A/B on one box):
+//   CH = 2: 11.53   CH = 3: 11.10   CH = 4: 11.24   CH = 5: 11.03
+// (at 2 waves per SIMD and 256 VGPRs CH = 4 and 5 were equal, 10.90 / 10.92).
+// The chunk loops are unrolled twice, not fully: at 168 VGPRs full unrolling
+// spills 68 VGPRs (276 B of scratch per lane), unroll 2 spills 28 (132 B):
+//   CH = 5, full unroll: 10.83   unroll 1: 10.61   unroll 2: 10.38 ms
+#ifndef NTM_N20_CH
+#define NTM_N20_CH 5
+#endif
+#ifndef NTM_N20_UNROLL
+#define NTM_N20_UNROLL 2
+#endif
+#if NTM_N20_UNROLL > 0
+#define NTM_CHUNK_UNROLL NTM_N20_UNROLL
+#endif
+// chunk loops with a runtime trip count are left alone (the pragma is a hint)
+#pragma clang diagnostic ignored "-Wpass-failed"
+#undef NTM_CH
+#define NTM_CH NTM_N20_CH
+#include "ntm_step.h"
+
+NTM_DEFINE_HORIZON_LAUNCHERS(20)

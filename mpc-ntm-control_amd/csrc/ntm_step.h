@@ -139,10 +139,15 @@ __device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x
 #ifndef NTM_HOT_WAVES_PER_EU
 #define NTM_HOT_WAVES_PER_EU 2
 #endif
+#ifndef NTM_N20_WAVES_PER_EU
+#define NTM_N20_WAVES_PER_EU (NTM_FAR_N20 ? 3 : 2)
+#endif
 // Long horizons (NN > 32): the LDS workspace already limits a CU to fewer waves
 // than SIMDs, so the register budget of one wave per SIMD costs no occupancy and
-// removes the spills of the fully unrolled horizon loops.
-#define NTM_WAVES_PER_EU(NN) ((NN) > 32 ? 1 : NTM_HOT_WAVES_PER_EU)
+// removes the spills of the fully unrolled horizon loops.  N = 20: three waves per
+// SIMD (the far workspace fits 12 scenarios per CU); 168 VGPRs spill ~60 of them,
+// and the third wave still wins (11.92 -> 11.03 ms per step-batch, A/B on one box).
+#define NTM_WAVES_PER_EU(NN) ((NN) > 32 ? 1 : ((NN) == 20 ? NTM_N20_WAVES_PER_EU : NTM_HOT_WAVES_PER_EU))
 template <int P, int NN, bool GEN>
 __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, int64_t B, const double* __restrict__ x_k,
                                                  double* __restrict__ rho, double* __restrict__ U_old,
@@ -247,11 +252,61 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_run(Prob pb, i
 
 }  // namespace
 
-// The N = 50 specialisation lives in ntm_n50.hip (its own translation unit);
-// these launch it (grid of one 64-lane block per scenario, lds bytes each).
-hipError_t ntm_launch_step_n50(const ntm::Prob& pb, int64_t B, const double* x_k, double* rho, double* U_old,
-                               double* U, double* x_pred, double* x_next, int32_t* exitflag, int32_t* inner_iters,
-                               int32_t* active_ws, size_t lds, hipStream_t st);
-hipError_t ntm_launch_run_n50(const ntm::Prob& pb, int64_t B, int k_sim, const double* x0, double* xk, double* uk,
-                              double* Uk, double* wpred, int32_t* exitflag, int32_t* inner_iters, size_t lds,
-                              hipStream_t st);
+// Launchers of one horizon's one-wave-per-scenario kernels (grid of one 64-lane
+// block per scenario, lds bytes each), instantiated by the translation unit that
+// owns that horizon (ntm_n20.hip, ntm_n50.hip: each sets its own LDS batch size)
+template <typename K>
+hipError_t ntm_lds_opt_in(K kern, size_t lds) {
+    if (lds <= 64 * 1024) return hipSuccess;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)lds);
+}
+template <int NN>
+hipError_t ntm_launch_step_tu(const ntm::Prob& pb, int64_t B, const double* x_k, double* rho, double* U_old,
+                              double* U, double* x_pred, double* x_next, int32_t* exitflag, int32_t* inner_iters,
+                              int32_t* active_ws, size_t lds, hipStream_t st) {
+    const bool gen = pb.g.phys_on || pb.g.dist_on;     // the generator's build only when it is used
+    hipError_t e = gen ? ntm_lds_opt_in(k_mpc_step<64, NN, true>, lds) : ntm_lds_opt_in(k_mpc_step<64, NN, false>, lds);
+    if (e != hipSuccess) return e;
+    if (B <= 0) return hipSuccess;
+    if (gen)
+        hipLaunchKernelGGL((k_mpc_step<64, NN, true>), dim3((unsigned)B), dim3(64), lds, st, pb, B, x_k, rho, U_old, U,
+                           x_pred, x_next, exitflag, inner_iters, active_ws);
+    else
+        hipLaunchKernelGGL((k_mpc_step<64, NN, false>), dim3((unsigned)B), dim3(64), lds, st, pb, B, x_k, rho, U_old,
+                           U, x_pred, x_next, exitflag, inner_iters, active_ws);
+    return hipGetLastError();
+}
+template <int NN>
+hipError_t ntm_launch_run_tu(const ntm::Prob& pb, int64_t B, int k_sim, const double* x0, double* xk, double* uk,
+                             double* Uk, double* wpred, int32_t* exitflag, int32_t* inner_iters, size_t lds,
+                             hipStream_t st) {
+    hipError_t e = ntm_lds_opt_in(k_mpc_run<64, NN>, lds);
+    if (e != hipSuccess) return e;
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL((k_mpc_run<64, NN>), dim3((unsigned)B), dim3(64), lds, st, pb, B, k_sim, x0, xk, uk, Uk, wpred,
+                       exitflag, inner_iters);
+    return hipGetLastError();
+}
+
+#define NTM_DECLARE_HORIZON_LAUNCHERS(NNV)                                                                         \
+    hipError_t ntm_launch_step_n##NNV(const ntm::Prob& pb, int64_t B, const double* x_k, double* rho,             \
+                                      double* U_old, double* U, double* x_pred, double* x_next, int32_t* exitflag, \
+                                      int32_t* inner_iters, int32_t* active_ws, size_t lds, hipStream_t st);       \
+    hipError_t ntm_launch_run_n##NNV(const ntm::Prob& pb, int64_t B, int k_sim, const double* x0, double* xk,     \
+                                     double* uk, double* Uk, double* wpred, int32_t* exitflag,                     \
+                                     int32_t* inner_iters, size_t lds, hipStream_t st);
+#define NTM_DEFINE_HORIZON_LAUNCHERS(NNV)                                                                          \
+    hipError_t ntm_launch_step_n##NNV(const ntm::Prob& pb, int64_t B, const double* x_k, double* rho,             \
+                                      double* U_old, double* U, double* x_pred, double* x_next, int32_t* exitflag, \
+                                      int32_t* inner_iters, int32_t* active_ws, size_t lds, hipStream_t st) {      \
+        return ntm_launch_step_tu<NNV>(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters,          \
+                                       active_ws, lds, st);                                                        \
+    }                                                                                                              \
+    hipError_t ntm_launch_run_n##NNV(const ntm::Prob& pb, int64_t B, int k_sim, const double* x0, double* xk,     \
+                                     double* uk, double* Uk, double* wpred, int32_t* exitflag,                     \
+                                     int32_t* inner_iters, size_t lds, hipStream_t st) {                           \
+        return ntm_launch_run_tu<NNV>(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st);        \
+    }
+NTM_DECLARE_HORIZON_LAUNCHERS(20)
+NTM_DECLARE_HORIZON_LAUNCHERS(50)
