@@ -849,11 +849,14 @@ __device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l) {
         else if (ph == 1) { g0 = 0.0; g1 = k.a22; }
         else { g0 = k.C1; g1 = k.C2; }
         const double c0 = (ph == 2) ? k.C1 : 0.0, c1 = (ph == 2) ? k.C2 : 0.0;
-        double* col = w.Gt() + w.gidx(2 * l, l) - 2 * l;   // col[r], r >= 2l (Gamma lanes)
+        // this lane's record, stage i at rec[st i]: its Gamma column (col[r], r >= 2l),
+        // its Phi column (stride 4) or Lambda; one address for the three kinds of
+        // lanes, so every step is one pair of stores with no divergent branches
+        double* const rec = gam ? w.Gt() + w.gidx(2 * l, l) - 2 * l : (ph < 2 ? w.Phi() + 2 * ph : w.Lam());
+        const int st = (gam || ph == 2) ? 2 : 4;
         auto put = [&](int i) {
-            if (gam) { col[2 * i] = g0; col[2 * i + 1] = g1; }
-            else if (ph < 2) { w.Phi()[4 * i + 2 * ph] = g0; w.Phi()[4 * i + 2 * ph + 1] = g1; }
-            else { w.Lam()[2 * i] = g0; w.Lam()[2 * i + 1] = g1; }
+            rec[st * i] = g0;
+            rec[st * i + 1] = g1;
         };
         put(gam ? l : 0);
         // fixed trip count (unrolls), branch-free: Gamma rows i <= l keep (B_l, 0) and
