@@ -339,8 +339,9 @@ def main():
                      "flop_counters": "solver counters of the K timed launches (ntm_ctx_set_stats on in the "
                                       "timed region)",
                      "hbm_algorithmic_bytes_per_launch": FL.hbm_bytes_per_step(N, workspace=True) * B,
-                     "note": "fp64 VALU work (DPP/LDS, no MFMA: DESIGN.md §6); peak = MI355X fp64 vector rate "
-                             "(78.6 TF, equal to the fp64 matrix rate)"},
+                     "note": ("fp64 VALU work (DPP/LDS, no MFMA at this horizon: DESIGN.md §6)" if N <= 32 else
+                              "fp64 VALU work plus GI's full Gram on V_MFMA_F64_16X16X4F64 (gram_mfma, DESIGN.md §6)")
+                             + "; peak = MI355X fp64 vector rate (78.6 TF, equal to the fp64 matrix rate)"},
         "solver": {"inner_iters_mean": r["inner_iters_mean"], "qp_per_step": r["qps"],
                    "warm_verify_per_step": r["tries"], "gi_solves_per_step": r["giruns"],
                    "gi_iters_per_step": r["Kgi"], "active_rows_per_qp": r["qact"], "state_rows_per_qp": r["sgen"],

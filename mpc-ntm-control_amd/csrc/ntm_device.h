@@ -410,6 +410,9 @@ __device__ __forceinline__ double coef_b(const Coef& k, double r3) { return k.bc
 #ifndef NTM_FAR_N20
 #define NTM_FAR_N20 1
 #endif
+#ifndef NTM_FAR_JB
+#define NTM_FAR_JB 0         // columns per trip of the bordered elimination's loads in the far block (0: two, loaded as used)
+#endif
 #ifndef NTM_FAR_COLMAJOR
 #define NTM_FAR_COLMAJOR 0   // 1: J, T and the bordered factor column-major in the far block (slower)
 #endif
@@ -959,12 +962,90 @@ __device__ __forceinline__ double dot_rows2(const double* a, const double* c, in
 }
 
 // ---------------------------------------------------------------------------
+// Gram of Gamma columns on the matrix cores (long horizons): for the columns
+// j_a = col_of(a), a < nc, S(a, c) = X_a' (I (x) Q) X_c with X_a = Gamma(:, j_a),
+// i.e. S = X' Y with Y = (I (x) Q) X, the (nc x 2N) x (2N x nc) contraction of
+// NTM_MPC_Sim.m:120 restricted to those columns.  V_MFMA_F64_16X16X4F64 on
+// 16 x 16 tiles, K = 4 rows of Gamma per instruction (2N / 4 steps; NN even):
+// lane l holds A = X(r, 16 t + (l & 15)) and B = Y(r, 16 t + (l & 15)) with
+// r = 4 s + (l >> 4), both from the two Gamma rows of stage r / 2 (two LDS
+// loads); the lower tile pairs accumulate in registers and put(a, c, S) takes
+// every entry a >= c (D layout: column l & 15, row (l >> 4) + 4 i).  Same terms
+// as qdot_rows / gram_rows, summed in the matrix core's order.  P = 64 only,
+// called in wave-uniform control flow.
+// ---------------------------------------------------------------------------
+typedef double ntm_d4 __attribute__((ext_vector_type(4)));
+#ifndef NTM_MFMA_FF
+#define NTM_MFMA_FF 0      // the re-solve's compact G~_FF (bordered path): measured slower, off
+#endif
+#ifndef NTM_MFMA_FULL
+#define NTM_MFMA_FULL 1    // GI's full G~
+#endif
+template <int NN, class W, class ColOf, class Put>
+__device__ __forceinline__ void gram_mfma(const Prob& pb, const W& w, int nc, ColOf col_of, Put put, int l) {
+    static_assert(NN > 0 && NN % 2 == 0, "gram_mfma: compile-time even horizon");
+    constexpr int TM = (NN + 15) / 16;                 // tiles of 16 columns
+    constexpr int NP = TM * (TM + 1) / 2;              // lower tile pairs
+    const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
+    const int li = l & 15, lk = l >> 4;
+    const int T = (nc + 15) >> 4;
+    int base[TM], r0[TM];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) {
+        const int a = 16 * t + li;
+        const bool on = a < nc;
+        const int j = on ? col_of(a) : 0;
+        base[t] = w.gidx(2 * j, j) - 2 * j;             // Gamma(r, j) = Gt[base + r], r >= 2j
+        r0[t] = on ? 2 * j : 2 * NN;                    // rows above the block diagonal are zero
+    }
+    ntm_d4 acc[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) acc[p] = ntm_d4{0.0, 0.0, 0.0, 0.0};
+    const double* const G = w.Gt();
+#pragma unroll 1
+    for (int s = 0; s < NN / 2; ++s) {                  // not unrolled: the accumulators stay the only long-lived registers
+        const int re = 4 * s + (lk & ~1);               // the even row of this lane's stage
+        double xa[TM], yb[TM];
+#pragma unroll
+        for (int t = 0; t < TM; ++t) {
+            const bool in = re >= r0[t];
+            const double x0 = in ? G[base[t] + re] : 0.0, x1 = in ? G[base[t] + re + 1] : 0.0;
+            xa[t] = (lk & 1) ? x1 : x0;
+            yb[t] = (lk & 1) ? (q10 * x0 + q11 * x1) : (q00 * x0 + q01 * x1);
+        }
+        int p = 0;
+#pragma unroll
+        for (int ta = 0; ta < TM; ++ta)
+#pragma unroll
+            for (int tc = 0; tc <= ta; ++tc, ++p)
+                if (ta < T) acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[ta], yb[tc], acc[p], 0, 0, 0);
+    }
+    int p = 0;
+#pragma unroll
+    for (int ta = 0; ta < TM; ++ta)
+#pragma unroll
+        for (int tc = 0; tc <= ta; ++tc, ++p) {
+            if (ta >= T) continue;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int a = 16 * ta + lk + 4 * i, c = 16 * tc + li;
+                if (a < nc && c <= a) put(a, c, acc[p][i]);
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------
 // condensed cost G = 2 Gamma' Om Gamma (lower triangle into dst, col-major),
 // F = 2 Gamma' Om (e - R)      NTM_MPC_Sim.m:120-121 (CANON D8, D12)
 // ---------------------------------------------------------------------------
 template <int P, class W>
 __device__ __forceinline__ void gram_rows(const Prob& pb, const W& w, double* dst, int l) {
     const int N = w.n(), LD = w.ldj();
+    if constexpr (NTM_MFMA_FULL && W::kNN > 32 && P == 64) {   // the matrix cores (gram_mfma)
+        gram_mfma<W::kNN>(pb, w, N, [](int a) { return a; }, [&](int j, int kk, double sg) { dst[j + kk * LD] = 2 * sg; },
+                          l);
+        return;
+    }
     const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
     // one (j, kk) entry per lane; fixed-trip masked dot (column reads below the
     // packed column start stay inside Gt, see StructRows::check)
@@ -2215,8 +2296,17 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     const bool fused = kAlwaysFused || ((nt + 1 <= RPL * P) && (nt * (nt + 1) / 2 + nt <= N * LDJ + (N + 1) * LD));
     double* const Lp = w.J();
     if (!sq && fused && l < nF) Lp[w.brow(nt) + w.bcol(l, nt)] = -gl;
-    // --- compact G~_FF: one (a, c) entry per lane (packed rows, or lower col-major in R) ---
-    {
+    // --- compact G~_FF: one (a, c) entry per lane (packed rows, or lower col-major in R);
+    //     on the matrix cores at long horizons (gram_mfma) ---
+    constexpr bool kMfmaGram = NTM_MFMA_FF && W::kNN > 32 && P == 64;
+    if constexpr (kMfmaGram) {
+        if (!sq)
+            gram_mfma<W::kNN>(pb, w, nF, [&](int a) { return w.fidx()[a]; },
+                              [&](int a, int c, double sg) {
+                                  Lp[w.brow(a) + w.bcol(c, nt)] = (2 * sg) * w.D()[w.fidx()[a]] * w.D()[w.fidx()[c]];
+                              },
+                              l);
+    } else {
         const int npair = sq ? 0 : nF * (nF + 1) / 2;
         for (int idx = l; idx < npair; idx += P) {
             int a = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
@@ -2420,6 +2510,39 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                     const int rr = (k + b2 < nt) ? k + b2 : nt;
                     prb[b2] = Lp + w.brow(rr);
                 }
+                if constexpr (W::kFar && NTM_FAR_JB > 0) {
+                    // far block (HBM): JB columns per trip for all of the lane's rows and
+                    // the KB pivot rows, every load issued before the first use (one
+                    // memory round trip per trip instead of one per column pair); the
+                    // column index is clamped to k (inside every live row and pivot row),
+                    // the terms past k are skipped, so each sum keeps its column order
+                    constexpr int JB = NTM_FAR_JB > 0 ? NTM_FAR_JB : 1;
+                    for (int j = 0; j < k; j += JB) {
+                        int cj[JB];
+#pragma unroll
+                        for (int u = 0; u < JB; ++u) cj[u] = w.bcol((j + u < k) ? j + u : k, nt);
+                        double av[RPL][JB], pv[KB][JB];
+#pragma unroll
+                        for (int r = 0; r < RPL; ++r)
+#pragma unroll
+                            for (int u = 0; u < JB; ++u) av[r][u] = live[r] ? myrow[r][cj[u]] : 0.0;
+#pragma unroll
+                        for (int b2 = 0; b2 < KB; ++b2)
+#pragma unroll
+                            for (int u = 0; u < JB; ++u) pv[b2][u] = prb[b2][cj[u]];
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int u = 0; u < JB; ++u) {
+                            if (j + u >= k) break;
+                            const double su = (j + u < kf) ? -1.0 : 1.0;
+#pragma unroll
+                            for (int r = 0; r < RPL; ++r)
+                                if (live[r])
+#pragma unroll
+                                    for (int b2 = 0; b2 < KB; ++b2) sacc[r][b2] += (su * av[r][u]) * pv[b2][u];
+                        }
+                    }
+                } else {
 #pragma unroll
                 for (int r = 0; r < RPL; ++r) {
                     if (!live[r]) continue;
@@ -2440,6 +2563,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                             sacc[r][b2] += in1 ? (s1 * a1) * p1[b2] : 0.0;
                         }
                     }
+                }
                 }
                 double Lc[RPL][KB];
 #pragma unroll

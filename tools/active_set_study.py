@@ -4,6 +4,7 @@ on the NumPy oracle (CPU).  The figures quoted in DESIGN.md §4 come from here.
     python tools/active_set_study.py hits   [scenarios] [steps] [N] [mode]
     python tools/active_set_study.py repair [scenarios] [steps] [N] [mode]
     python tools/active_set_study.py shape  [scenarios] [steps] [N] [mode]
+    python tools/active_set_study.py collide [scenarios] [steps] [N] [mode]
 
 hits   - how often the previous step's last odd / even active set (carried
          unshifted or shifted by one stage) equals the set of inner iteration 1 / 2,
@@ -12,6 +13,7 @@ repair - of the misses, how many single-row repairs recover the optimal set
          (exact active-set solves), without and with the bound-row swap
 shape  - the shape of the optimal sets: echelon (every general row ends in its
          own free column) and the null-space dimension k = n_F - n_S
+collide - the non-echelon optimal sets by k, collisions and bordered size n_F + n_S
 Steps 0-4 are the transient ("early"), later steps the steady state ("late").
 """
 import sys
@@ -101,6 +103,32 @@ def shape(Lin, S, N):
     return (len(set(last)) == len(gen) and min(last) >= 0), len(free) - len(gen)
 
 
+def collisions(Lin, S, N):
+    """Non-echelon optimal sets: (k = n_F - n_S, collisions = rows that do not own their
+    last free column, n_F + n_S, whether the square E (k = 0) is nonsingular)."""
+    fixed, gen = set(), []
+    for r in sorted(S):
+        nz = np.flatnonzero(Lin[r])
+        (fixed.add(nz[0]) if len(nz) == 1 else gen.append(r))
+    free = [j for j in range(N) if j not in fixed]
+    if not gen:
+        return [("all",)]
+    E = Lin[np.ix_(gen, free)]
+    last = [max((a for a in range(len(free)) if E[i, a] != 0), default=-1) for i in range(len(gen))]
+    ncol = len(gen) - len(set(last))
+    kk = len(free) - len(gen)
+    out = [("all",)]
+    if ncol == 0 and min(last) >= 0:
+        out.append(("echelon", f"k={kk}"))
+    else:
+        sing = ""
+        if kk == 0:
+            sing = "E nonsingular" if np.linalg.matrix_rank(E) == len(gen) else "E singular"
+        out.append(("not echelon", f"k={kk}", f"collisions={min(ncol, 4)}", sing))
+        out.append(("not echelon nt", f"nt<=40" if len(free) + len(gen) <= 40 else ("nt<=61" if len(free) + len(gen) <= 61 else "nt>61")))
+    return out
+
+
 def main():
     what = sys.argv[1]
     ns, K = int(sys.argv[2]) if len(sys.argv) > 2 else 12, int(sys.argv[3]) if len(sys.argv) > 3 else 20
@@ -137,6 +165,9 @@ def main():
                 elif what == "shape" and k >= 3:
                     ech, kk = shape(Lin, S, N)
                     cnt[("echelon" if ech else "not echelon", f"k={kk}" if ech else "")] += 1
+                elif what == "collide" and k >= 3:
+                    for key in collisions(Lin, S, N):
+                        cnt[key] += 1
                 _, Rho = O.rollout(xk, Rho, U, ph, cfg)
                 if np.sum(np.abs(Uold - U)) < cfg.epsilon:
                     break

@@ -11,6 +11,8 @@ import sys
 from pathlib import Path
 
 outdir, tag = Path(sys.argv[1]), sys.argv[2]
+# resident waves per SIMD of the measured build (N=20: 3 since the far workspace, round 3; 2 before)
+wps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 
 
 def last_step(path):
@@ -40,8 +42,8 @@ res = {
         "parked_waitcnt_frac_of_wave_cycles": c.get("SQ_WAIT_ANY", 0.0) / wc if wc else None,
         "issue_stall_frac_of_wave_cycles": c.get("SQ_WAIT_INST_ANY", 0.0) / wc if wc else None,
         "fp64_arith_frac_of_valu_insts": f64 / valu if valu else None,
-        "waves_per_simd": 2,
-        "simd_valu_busy_estimate": 2 * c.get("SQ_ACTIVE_INST_VALU", 0.0) / wc if wc else None,
+        "waves_per_simd": wps,
+        "simd_valu_busy_estimate": wps * c.get("SQ_ACTIVE_INST_VALU", 0.0) / wc if wc else None,
     },
     "note": "separate --pmc passes (8 SQ counters each) over one bench step at B=1e5, N=20; the "
             "SIMD VALU busy estimate is waves/SIMD x the per-wave VALU-issue fraction.",
