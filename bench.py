@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--no-stats", action="store_true",
                     help="A/B only: leave the solver counters off in the timed region (roofline then unavailable)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample length")
+    ap.add_argument("--small-batch", type=int, default=-1,
+                    help="N=20: batches up to this size run on the all-LDS build (-1: library default, 0: never)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse the multi-rank "
                          "control flow with more ranks than GPUs (ranks share devices, timing not meaningful)")
@@ -236,8 +238,15 @@ def _verify_gathered(ctl, cfg, B_total, K, W, g, n_verify, seed=12345):
     x0 = np.concatenate([ntm_mpc.scenarios_x0(int(i), 1) for i in ids], axis=1)
     x = ctl.tensor(x0)
     n = len(ids)
-    leg = _run_leg(ctl, cfg, n, K, W, x, 0, 1, collect=True)
-    _finish_leg(ctl, leg, K)
+    # the recompute takes the build the gathered run took (the library picks the
+    # N = 20 build by batch size; bitwise equality holds within one build)
+    ctl.set_small_batch(1 << 62 if ctl.step_layout(B_total // int(os.environ.get("WORLD_SIZE", "1")), cfg) == "lds"
+                        else 0)
+    try:
+        leg = _run_leg(ctl, cfg, n, K, W, x, 0, 1, collect=True)
+        _finish_leg(ctl, leg, K)
+    finally:
+        ctl.set_small_batch(-1)
     sel = torch.as_tensor(ids, device=leg["hist"]["uk"].device)
     bad = [k for k, v in leg["hist"].items() if not bool((v == g[k].index_select(-1, sel)).all().item())]
     return {"scenarios": n, "ids_seed": seed, "bitwise_equal": not bad, "mismatched": bad}
@@ -269,6 +278,7 @@ def main():
     B, N, K, W = args.batch, args.N, args.steps, args.warmup
     cfg = Config(N=N, mode=args.mode)
     ctl = NtmMpc(config=cfg, device=local)
+    ctl.set_small_batch(args.small_batch)
     # shard: global scenario ids [rank*B, (rank+1)*B)  (shard-invariant inputs)
     x0 = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(rank * B, B), local)
 

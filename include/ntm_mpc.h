@@ -102,6 +102,17 @@ const char* ntm_last_error(const ntm_ctx* ctx);
  * 5 full Goldfarb-Idnani solves.  NULL disables. */
 #define NTM_STATS_ROWS 6
 int ntm_ctx_set_stats(ntm_ctx* ctx, int32_t* dev_stats);
+/* Workspace layout of the N = 20 step/run kernels by batch size: batches of at
+ * most max_scenarios run on the all-LDS build (2 waves per SIMD), larger ones on
+ * the far-workspace build (3 waves per SIMD, GI factors in a per-scenario HBM
+ * block).  Default (and max_scenarios < 0): 32 x the device's compute units, the
+ * measured crossover (8192 on an MI355X); 0 = always the far build.  Results of
+ * the two builds agree to the parity tolerances, not bit for bit; within one
+ * build a scenario's results do not depend on the batch around it. */
+int ntm_ctx_set_small_batch(ntm_ctx* ctx, int64_t max_scenarios);
+/* Which build a step/run launch of B scenarios at horizon N takes on this
+ * context: *far = 1 for the far-workspace build, 0 for an all-LDS one. */
+int ntm_ctx_step_layout(const ntm_ctx* ctx, int32_t N, int64_t B, int32_t* far);
 /* Diagnostic builds only: per-phase s_memtime cycle totals (48 counters);
  * NTM_E_UNSUPPORTED in production builds. */
 int ntm_debug_stamps(unsigned long long* out32, int reset);

@@ -418,11 +418,11 @@ __device__ __forceinline__ double coef_b(const Coef& k, double r3) { return k.bc
 #endif
 __host__ __device__ constexpr bool ws_far(int NN) { return NN > 32 || (NTM_FAR_N20 && NN == 20); }
 
-template <int NN, bool GEN = false>
+template <int NN, bool GEN = false, bool FAR = ws_far(NN)>
 struct WS {
     static constexpr int kNN = NN;
     static constexpr bool kGen = GEN;
-    static constexpr bool kFar = ws_far(NN);
+    static constexpr bool kFar = FAR;
     int N_rt;
     double* base;
     double* far;       // kFar: this scenario's J/R block in HBM
@@ -553,13 +553,13 @@ __host__ __device__ inline int ws_bytes_rows(int N, int rows, bool far = false) 
 __host__ __device__ inline int ws_bytes(int N, bool far = false) { return ws_bytes_rows(N, 8 * N + 4, far); }
 
 // s: the scenario's index in the launch (its far block, when the WS has one)
-template <int NN, bool GEN = false>
-__device__ inline WS<NN, GEN> ws_carve(char* base, int N, const Prob* pb = nullptr, int64_t s = 0) {
-    WS<NN, GEN> w;
+template <int NN, bool GEN = false, bool FAR = ws_far(NN)>
+__device__ inline WS<NN, GEN, FAR> ws_carve(char* base, int N, const Prob* pb = nullptr, int64_t s = 0) {
+    WS<NN, GEN, FAR> w;
     w.N_rt = N;
     w.base = reinterpret_cast<double*>(base);
     w.far = nullptr;
-    if constexpr (WS<NN, GEN>::kFar) w.far = pb->far + s * (int64_t)far_doubles(N);
+    if constexpr (FAR) w.far = pb->far + s * (int64_t)far_doubles(N);
     return w;
 }
 

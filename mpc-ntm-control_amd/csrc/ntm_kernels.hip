@@ -398,6 +398,8 @@ struct ntm_ctx {
     void* fbuf = nullptr;       // far workspaces of the long-horizon kernels (ws_far)
     size_t fbuf_bytes = 0;
     hipEvent_t fbuf_done = nullptr;   // recorded after the last launch that used fbuf
+    int cus = 256;                    // compute units of the device (small_batch)
+    int64_t near_max = -1;            // ntm_ctx_set_small_batch (< 0: 32 x cus)
     hipStream_t stream = nullptr;
 };
 
@@ -497,27 +499,54 @@ int far_release(ntm_ctx* ctx, int rc, hipStream_t st) {
 }
 
 
+// N = 20 batches up to 32 scenarios per CU (four rounds of the all-LDS 2-wave
+// build, which holds 8 per CU at once) run on that build: each of its waves is
+// faster than the far 3-wave build's, whose extra occupancy such a batch cannot
+// use for long (measured, steps 6-25, mode 2: B = 1024 0.74 vs 0.92 ms, 8192 1.49
+// vs 1.51, 16384 2.41 vs 2.26, 65536 7.94 vs 6.85; BASELINE config 2: B = 1024).
+// ntm_ctx_set_small_batch overrides the threshold (0: always the far build).
+template <int NN>
+bool small_batch(const ntm_ctx* ctx, int64_t B) {
+    if constexpr (NN != 20 || !ws_far(NN)) {
+        return false;
+    } else {
+        const int64_t lim = ctx->near_max >= 0 ? ctx->near_max : 32LL * ctx->cus;
+        return B <= lim;
+    }
+}
+
 template <int P, int NN>
 int launch_step(ntm_ctx* ctx, Prob pb, int64_t B, const double* x_k, double* rho, double* U_old,
                 double* U, double* x_pred, double* x_next, int32_t* exitflag, int32_t* inner_iters,
                 int32_t* active_ws, hipStream_t st) {
     constexpr int G = 64 / P;
-    size_t lds = (size_t)G * ws_bytes(pb.N, ws_far(NN));
-    if (int rc = attach_far<NN>(ctx, pb, B, st)) return rc;
-#ifdef NTM_LDS_PAD
-    lds += NTM_LDS_PAD;   // occupancy study only (tools/occupancy_study.sh): fewer scenarios per CU
-#endif
 #ifndef NTM_SINGLE_TU
     if constexpr (P == 64 && (NN == 20 || NN == 50)) {   // ntm_n20.hip, ntm_n50.hip
+        const bool near = small_batch<NN>(ctx, B);
+        size_t lds = (size_t)G * ws_bytes(pb.N, ws_far(NN) && !near);
+#ifdef NTM_LDS_PAD
+        lds += NTM_LDS_PAD;   // occupancy study only (tools/occupancy_study.sh): fewer scenarios per CU
+#endif
         if (lds > 160 * 1024) return fail(ctx, NTM_E_UNSUPPORTED, "LDS workspace exceeds 160 KiB");
-        const hipError_t e = NN == 20 ? ntm_launch_step_n20(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag,
-                                                            inner_iters, active_ws, lds, st)
-                                      : ntm_launch_step_n50(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag,
-                                                            inner_iters, active_ws, lds, st);
-        return far_release<NN>(ctx, check_hip(ctx, e, "k_mpc_step<64,NN> launch"), st);
+        if (!near)
+            if (int rc = attach_far<NN>(ctx, pb, B, st)) return rc;
+        const hipError_t e =
+            NN == 50 ? ntm_launch_step_n50(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, active_ws,
+                                           lds, st)
+            : near   ? ntm_launch_step_n20near(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters,
+                                               active_ws, lds, st)
+                     : ntm_launch_step_n20(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, active_ws,
+                                           lds, st);
+        const int rc = check_hip(ctx, e, "k_mpc_step<64,NN> launch");
+        return near ? rc : far_release<NN>(ctx, rc, st);
     } else
 #endif
     {
+    size_t lds = (size_t)G * ws_bytes(pb.N, ws_far(NN));
+    if (int rc = attach_far<NN>(ctx, pb, B, st)) return rc;
+#ifdef NTM_LDS_PAD
+    lds += NTM_LDS_PAD;
+#endif
     const bool gen = pb.g.phys_on || pb.g.dist_on;     // the generator's build only when it is used
     int rc = gen ? set_lds(ctx, k_mpc_step<P, NN, true>, lds) : set_lds(ctx, k_mpc_step<P, NN, false>, lds);
     if (rc) return rc;
@@ -537,18 +566,24 @@ template <int P, int NN>
 int launch_run(ntm_ctx* ctx, Prob pb, int64_t B, int k_sim, const double* x0, double* xk, double* uk,
                double* Uk, double* wpred, int32_t* exitflag, int32_t* inner_iters, hipStream_t st) {
     constexpr int G = 64 / P;
-    size_t lds = (size_t)G * ws_bytes(pb.N, ws_far(NN));
-    if (int rc = attach_far<NN>(ctx, pb, B, st)) return rc;
 #ifndef NTM_SINGLE_TU
     if constexpr (P == 64 && (NN == 20 || NN == 50)) {   // ntm_n20.hip, ntm_n50.hip
+        const bool near = small_batch<NN>(ctx, B);
+        const size_t lds = (size_t)G * ws_bytes(pb.N, ws_far(NN) && !near);
         if (lds > 160 * 1024) return fail(ctx, NTM_E_UNSUPPORTED, "LDS workspace exceeds 160 KiB");
+        if (!near)
+            if (int rc = attach_far<NN>(ctx, pb, B, st)) return rc;
         const hipError_t e =
-            NN == 20 ? ntm_launch_run_n20(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st)
-                     : ntm_launch_run_n50(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st);
-        return far_release<NN>(ctx, check_hip(ctx, e, "k_mpc_run<64,NN> launch"), st);
+            NN == 50 ? ntm_launch_run_n50(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st)
+            : near   ? ntm_launch_run_n20near(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st)
+                     : ntm_launch_run_n20(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st);
+        const int rc = check_hip(ctx, e, "k_mpc_run<64,NN> launch");
+        return near ? rc : far_release<NN>(ctx, rc, st);
     } else
 #endif
     {
+    const size_t lds = (size_t)G * ws_bytes(pb.N, ws_far(NN));
+    if (int rc = attach_far<NN>(ctx, pb, B, st)) return rc;
     int rc = set_lds(ctx, k_mpc_run<P, NN>, lds);
     if (rc) return rc;
     int64_t blocks = (B + G - 1) / G;
@@ -665,6 +700,10 @@ int ntm_ctx_create(ntm_ctx** out, int32_t device) {
         if (hipGetDevice(&cur) != hipSuccess || cur != device ||
             hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
             rc = NTM_E_DEVICE;
+        int cus = 0;
+        if (rc == NTM_OK && hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+            cus > 0)
+            c->cus = cus;
     }
     if (rc != NTM_OK) {
         delete c;
@@ -707,6 +746,22 @@ int ntm_debug_stamps(unsigned long long* out32, int reset) {
 int ntm_ctx_set_stats(ntm_ctx* ctx, int32_t* dev_stats) {
     if (!ctx) return NTM_E_INVALID;
     ctx->stats = dev_stats;
+    return NTM_OK;
+}
+
+int ntm_ctx_set_small_batch(ntm_ctx* ctx, int64_t max_scenarios) {
+    if (!ctx) return NTM_E_INVALID;
+    ctx->near_max = max_scenarios < 0 ? -1 : max_scenarios;
+    return NTM_OK;
+}
+
+int ntm_ctx_step_layout(const ntm_ctx* ctx, int32_t N, int64_t B, int32_t* far) {
+    if (!ctx || !far || N < 1 || N > NTM_MAX_N || B < 0) return NTM_E_INVALID;
+    int32_t lanes = 0, nn = 0;
+    (void)ntm_step_launch_info(N, &lanes, &nn);
+    *far = (lanes == 64 && nn == 20) ? (small_batch<20>(ctx, B) ? 0 : (ws_far(20) ? 1 : 0))
+           : (lanes == 64 && nn == 50) ? (ws_far(50) ? 1 : 0)
+                                       : 0;
     return NTM_OK;
 }
 

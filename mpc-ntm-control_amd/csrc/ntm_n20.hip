@@ -22,4 +22,4 @@
 #define NTM_CH NTM_N20_CH
 #include "ntm_step.h"
 
-NTM_DEFINE_HORIZON_LAUNCHERS(20)
+NTM_DEFINE_LAYOUT_LAUNCHERS(n20, 20, true)

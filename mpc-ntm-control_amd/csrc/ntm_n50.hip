@@ -16,4 +16,4 @@
 #define NTM_CH NTM_N50_CH
 #include "ntm_step.h"
 
-NTM_DEFINE_HORIZON_LAUNCHERS(50)
+NTM_DEFINE_LAYOUT_LAUNCHERS(n50, 50, true)

@@ -147,9 +147,13 @@ __device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x
 // removes the spills of the fully unrolled horizon loops.  N = 20: three waves per
 // SIMD (the far workspace fits 12 scenarios per CU); 168 VGPRs spill ~60 of them,
 // and the third wave still wins (11.92 -> 11.03 ms per step-batch, A/B on one box).
-#define NTM_WAVES_PER_EU(NN) ((NN) > 32 ? 1 : ((NN) == 20 ? NTM_N20_WAVES_PER_EU : NTM_HOT_WAVES_PER_EU))
-template <int P, int NN, bool GEN>
-__global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, int64_t B, const double* __restrict__ x_k,
+// FAR = false at N = 20: the all-LDS build (2 waves per SIMD, 256 VGPRs), which
+// runs each wave faster and is launched for batches that fill no more than its
+// 8 scenarios per CU (small_batch in ntm_kernels.hip)
+#define NTM_WAVES_PER_EU(NN, FAR) \
+    ((NN) > 32 ? 1 : ((NN) == 20 && (FAR) ? NTM_N20_WAVES_PER_EU : NTM_HOT_WAVES_PER_EU))
+template <int P, int NN, bool GEN, bool FAR = ws_far(NN)>
+__global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN, FAR)) void k_mpc_step(Prob pb, int64_t B, const double* __restrict__ x_k,
                                                  double* __restrict__ rho, double* __restrict__ U_old,
                                                  double* __restrict__ U, double* __restrict__ x_pred,
                                                  double* __restrict__ x_next, int32_t* __restrict__ exitflag,
@@ -162,12 +166,12 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, 
     NTM_STAMPS_INIT();
     NTM_TRACE_SET(s, g, l);
     if (s >= B) return;
-    auto w = ws_carve<NN, GEN>(smem + g * ws_bytes(N, ws_far(NN)), N, &pb, s);
+    auto w = ws_carve<NN, GEN, FAR>(smem + g * ws_bytes(N, FAR), N, &pb, s);
 #ifdef NTM_POISON
     // debug build (make poison): the workspace starts as NTM_POISON-valued doubles, so
     // a read of LDS this launch never wrote shows up as a run-to-run difference
     // (tools/determinism.py + compare_runs.py; this found the x_0-row read of rinfo[-1])
-    for (int e = l; e < ws_bytes(N, ws_far(NN)) / 8; e += P) w.base[e] = NTM_POISON;
+    for (int e = l; e < ws_bytes(N, FAR) / 8; e += P) w.base[e] = NTM_POISON;
     NTM_WSYNC();
 #endif
     const double x0 = x_k[2 * s], x1 = x_k[2 * s + 1];
@@ -204,8 +208,8 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_step(Prob pb, 
     NTM_STAMPS_FLUSH();
 }
 
-template <int P, int NN>
-__global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_run(Prob pb, int64_t B, int k_sim, const double* __restrict__ x0v,
+template <int P, int NN, bool FAR = ws_far(NN)>
+__global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN, FAR)) void k_mpc_run(Prob pb, int64_t B, int k_sim, const double* __restrict__ x0v,
                                                 double* xk, double* uk, double* Uk, double* wpred,
                                                 int32_t* exitflag, int32_t* inner_iters) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -214,7 +218,7 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN)) void k_mpc_run(Prob pb, i
     const int64_t s = xcd_swizzle(blockIdx.x, gridDim.x) * G + g;
     const int N = NN > 0 ? NN : pb.N;
     if (s >= B) return;
-    auto w = ws_carve<NN, true>(smem + g * ws_bytes(N, ws_far(NN)), N, &pb, s);
+    auto w = ws_carve<NN, true, FAR>(smem + g * ws_bytes(N, FAR), N, &pb, s);
     double x0 = x0v[2 * s], x1 = x0v[2 * s + 1];
     if (l < 2) w.cand()[l * (N + 1) + N] = -1;
     scn_store(pb, w, pb.g.first_id + s, l);           // this scenario's plasma (generator)
@@ -261,52 +265,55 @@ hipError_t ntm_lds_opt_in(K kern, size_t lds) {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)lds);
 }
-template <int NN>
-hipError_t ntm_launch_step_tu(const ntm::Prob& pb, int64_t B, const double* x_k, double* rho, double* U_old,
-                              double* U, double* x_pred, double* x_next, int32_t* exitflag, int32_t* inner_iters,
-                              int32_t* active_ws, size_t lds, hipStream_t st) {
+template <int NN, bool FAR>
+hipError_t ntm_launch_step_v(const ntm::Prob& pb, int64_t B, const double* x_k, double* rho, double* U_old, double* U,
+                             double* x_pred, double* x_next, int32_t* exitflag, int32_t* inner_iters,
+                             int32_t* active_ws, size_t lds, hipStream_t st) {
     const bool gen = pb.g.phys_on || pb.g.dist_on;     // the generator's build only when it is used
-    hipError_t e = gen ? ntm_lds_opt_in(k_mpc_step<64, NN, true>, lds) : ntm_lds_opt_in(k_mpc_step<64, NN, false>, lds);
+    hipError_t e = gen ? ntm_lds_opt_in(k_mpc_step<64, NN, true, FAR>, lds)
+                       : ntm_lds_opt_in(k_mpc_step<64, NN, false, FAR>, lds);
     if (e != hipSuccess) return e;
     if (B <= 0) return hipSuccess;
     if (gen)
-        hipLaunchKernelGGL((k_mpc_step<64, NN, true>), dim3((unsigned)B), dim3(64), lds, st, pb, B, x_k, rho, U_old, U,
-                           x_pred, x_next, exitflag, inner_iters, active_ws);
+        hipLaunchKernelGGL((k_mpc_step<64, NN, true, FAR>), dim3((unsigned)B), dim3(64), lds, st, pb, B, x_k, rho,
+                           U_old, U, x_pred, x_next, exitflag, inner_iters, active_ws);
     else
-        hipLaunchKernelGGL((k_mpc_step<64, NN, false>), dim3((unsigned)B), dim3(64), lds, st, pb, B, x_k, rho, U_old,
-                           U, x_pred, x_next, exitflag, inner_iters, active_ws);
+        hipLaunchKernelGGL((k_mpc_step<64, NN, false, FAR>), dim3((unsigned)B), dim3(64), lds, st, pb, B, x_k, rho,
+                           U_old, U, x_pred, x_next, exitflag, inner_iters, active_ws);
     return hipGetLastError();
 }
-template <int NN>
-hipError_t ntm_launch_run_tu(const ntm::Prob& pb, int64_t B, int k_sim, const double* x0, double* xk, double* uk,
-                             double* Uk, double* wpred, int32_t* exitflag, int32_t* inner_iters, size_t lds,
-                             hipStream_t st) {
-    hipError_t e = ntm_lds_opt_in(k_mpc_run<64, NN>, lds);
+template <int NN, bool FAR>
+hipError_t ntm_launch_run_v(const ntm::Prob& pb, int64_t B, int k_sim, const double* x0, double* xk, double* uk,
+                            double* Uk, double* wpred, int32_t* exitflag, int32_t* inner_iters, size_t lds,
+                            hipStream_t st) {
+    hipError_t e = ntm_lds_opt_in(k_mpc_run<64, NN, FAR>, lds);
     if (e != hipSuccess) return e;
     if (B <= 0) return hipSuccess;
-    hipLaunchKernelGGL((k_mpc_run<64, NN>), dim3((unsigned)B), dim3(64), lds, st, pb, B, k_sim, x0, xk, uk, Uk, wpred,
-                       exitflag, inner_iters);
+    hipLaunchKernelGGL((k_mpc_run<64, NN, FAR>), dim3((unsigned)B), dim3(64), lds, st, pb, B, k_sim, x0, xk, uk, Uk,
+                       wpred, exitflag, inner_iters);
     return hipGetLastError();
 }
-
-#define NTM_DECLARE_HORIZON_LAUNCHERS(NNV)                                                                         \
-    hipError_t ntm_launch_step_n##NNV(const ntm::Prob& pb, int64_t B, const double* x_k, double* rho,             \
+// One translation unit per (horizon, layout): ntm_n20.hip (far), ntm_n20near.hip (the
+// all-LDS N = 20 build for small batches, its own batch settings), ntm_n50.hip (far)
+#define NTM_DECLARE_LAYOUT_LAUNCHERS(NAME)                                                                         \
+    hipError_t ntm_launch_step_##NAME(const ntm::Prob& pb, int64_t B, const double* x_k, double* rho,             \
                                       double* U_old, double* U, double* x_pred, double* x_next, int32_t* exitflag, \
                                       int32_t* inner_iters, int32_t* active_ws, size_t lds, hipStream_t st);       \
-    hipError_t ntm_launch_run_n##NNV(const ntm::Prob& pb, int64_t B, int k_sim, const double* x0, double* xk,     \
+    hipError_t ntm_launch_run_##NAME(const ntm::Prob& pb, int64_t B, int k_sim, const double* x0, double* xk,     \
                                      double* uk, double* Uk, double* wpred, int32_t* exitflag,                     \
                                      int32_t* inner_iters, size_t lds, hipStream_t st);
-#define NTM_DEFINE_HORIZON_LAUNCHERS(NNV)                                                                          \
-    hipError_t ntm_launch_step_n##NNV(const ntm::Prob& pb, int64_t B, const double* x_k, double* rho,             \
+#define NTM_DEFINE_LAYOUT_LAUNCHERS(NAME, NNV, FARV)                                                               \
+    hipError_t ntm_launch_step_##NAME(const ntm::Prob& pb, int64_t B, const double* x_k, double* rho,             \
                                       double* U_old, double* U, double* x_pred, double* x_next, int32_t* exitflag, \
                                       int32_t* inner_iters, int32_t* active_ws, size_t lds, hipStream_t st) {      \
-        return ntm_launch_step_tu<NNV>(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters,          \
-                                       active_ws, lds, st);                                                        \
+        return ntm_launch_step_v<NNV, FARV>(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters,     \
+                                            active_ws, lds, st);                                                   \
     }                                                                                                              \
-    hipError_t ntm_launch_run_n##NNV(const ntm::Prob& pb, int64_t B, int k_sim, const double* x0, double* xk,     \
+    hipError_t ntm_launch_run_##NAME(const ntm::Prob& pb, int64_t B, int k_sim, const double* x0, double* xk,     \
                                      double* uk, double* Uk, double* wpred, int32_t* exitflag,                     \
                                      int32_t* inner_iters, size_t lds, hipStream_t st) {                           \
-        return ntm_launch_run_tu<NNV>(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st);        \
+        return ntm_launch_run_v<NNV, FARV>(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st);  \
     }
-NTM_DECLARE_HORIZON_LAUNCHERS(20)
-NTM_DECLARE_HORIZON_LAUNCHERS(50)
+NTM_DECLARE_LAYOUT_LAUNCHERS(n20)
+NTM_DECLARE_LAYOUT_LAUNCHERS(n20near)
+NTM_DECLARE_LAYOUT_LAUNCHERS(n50)

@@ -248,6 +248,13 @@ class NtmMpc:
             _check_dev(stats, tuple(stats.shape), dtype=torch.int32, name="stats")
         self._raise(self.lib.ntm_ctx_set_stats(self._ctx, _ptr(stats)), "ntm_ctx_set_stats")
 
+    def set_small_batch(self, max_scenarios: int = -1):
+        """ntm_ctx_set_small_batch: N = 20 batches of at most ``max_scenarios``
+        run on the all-LDS 2-wave build, larger ones on the far-workspace 3-wave
+        build; -1 restores the default (32 x the compute units), 0 always uses
+        the far build."""
+        self._raise(self.lib.ntm_ctx_set_small_batch(self._ctx, int(max_scenarios)), "ntm_ctx_set_small_batch")
+
     def set_scenarios(self, gen: ScenarioGen | None):
         """Attach a scenario generator (ntm_ctx_set_scenarios): subsequent
         initial_state / step / run launches use each scenario's own plasma and
@@ -257,12 +264,20 @@ class NtmMpc:
         self._raise(self.lib.ntm_ctx_set_scenarios(self._ctx, None if gen is None else C.byref(gen.to_c())),
                     "ntm_ctx_set_scenarios")
 
+    def step_layout(self, B: int, cfg: Config | None = None) -> str:
+        """Workspace layout of the build a launch of B scenarios takes: "far"
+        (J/R in a per-scenario HBM block) or "lds" (ntm_ctx_step_layout)."""
+        cfg = cfg or self.config
+        far = C.c_int32()
+        self._raise(self.lib.ntm_ctx_step_layout(self._ctx, cfg.N, int(B), C.byref(far)), "ntm_ctx_step_layout")
+        return "far" if far.value else "lds"
+
     def step_kernel_name(self, B: int, cfg: Config | None = None) -> str:
         """Name of the fused step kernel specialisation a launch uses (reporting)."""
         cfg = cfg or self.config
         lanes, nn = C.c_int32(), C.c_int32()
         self._raise(self.lib.ntm_step_launch_info(cfg.N, C.byref(lanes), C.byref(nn)), "ntm_step_launch_info")
-        return f"k_mpc_step<P={lanes.value},NN={nn.value}>"
+        return f"k_mpc_step<P={lanes.value},NN={nn.value},{self.step_layout(B, cfg)}>"
 
     # ------------------------------------------------------------ hot path
     def initial_state(self, x0: torch.Tensor, cfg: Config | None = None):

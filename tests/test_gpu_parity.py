@@ -202,6 +202,72 @@ def test_step_teacher_forced_weighted(ctl, N, mode, warm):
     _teacher_forced(ctl, N, mode, warm, k_sim=6, Q=(2.0e4, 3.0, 3.0, 2.0e-2), r=(0.09, 900 * 2 * math.pi))
 
 
+# N = 20 has two builds (ntm_ctx_set_small_batch): batches up to 32 x the compute
+# units (8192 on an MI355X) run on the all-LDS 2-wave build, which is what the
+# small batches of these tests reach by default; larger ones on the far-workspace
+# 3-wave build (GI's factors in HBM), forced here.  The full-size tests
+# (test_full_size_batch_properties) run the far build at B = 1e5 by default.
+@pytest.mark.parametrize("N,mode,warm", [(20, 1, False), (20, 2, False), (20, 2, True), (20, 3, True)])
+def test_step_teacher_forced_far_build(ctl, N, mode, warm):
+    ctl.set_small_batch(0)
+    try:
+        _teacher_forced(ctl, N, mode, warm)
+    finally:
+        ctl.set_small_batch(-1)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_run_closed_loop_far_build(ctl, mode):
+    B, k_sim = 32, 20
+    cfg, ocfg = cfgs(20, mode)
+    x0 = O.scenario_x0(np.arange(B)).T
+    ref = cbind.run(x0, ocfg, k_sim)
+    ctl.set_small_batch(0)
+    try:
+        out = ctl.run(T(x0), k_sim, cfg)
+    finally:
+        ctl.set_small_batch(-1)
+    _assert_run_close(out, ref, cfg, k_sim)
+
+
+def test_step_layout_by_batch(ctl):
+    """ntm_ctx_step_layout reports the build ntm_ctx_set_small_batch selects."""
+    from ntm_mpc import Config
+    c20, c50, c10 = Config(N=20, mode=2), Config(N=50, mode=2), Config(N=10, mode=2)
+    assert ctl.step_layout(1024, c20) == "lds" and ctl.step_layout(100_000, c20) == "far"
+    assert ctl.step_layout(100_000, c50) == "far" and ctl.step_layout(1, c50) == "far"
+    assert ctl.step_layout(100_000, c10) == "lds"
+    ctl.set_small_batch(0)
+    try:
+        assert ctl.step_layout(1, c20) == "far"
+        ctl.set_small_batch(1 << 40)
+        assert ctl.step_layout(100_000, c20) == "lds"
+    finally:
+        ctl.set_small_batch(-1)
+
+
+def test_small_batch_builds_agree(ctl):
+    """The two N = 20 builds on the same inputs: same flags and inner iterations,
+    U to 1e-12 umax (same arithmetic in different register allocations; the
+    bitwise stopping rule could still part them by an iteration, which these
+    seeded inputs do not)."""
+    B = 256
+    cfg, ocfg = cfgs(20, 2)
+    x = O.scenario_x0(np.arange(B)).T
+    rho, Uo = cbind.initial_state(x, ocfg)
+    outs = []
+    for lim in (-1, 0):
+        ctl.set_small_batch(lim)
+        try:
+            outs.append(ctl.step(T(x), T(rho), T(Uo), cfg))
+        finally:
+            ctl.set_small_batch(-1)
+    a, b = outs
+    assert (H(a["exitflag"]) == H(b["exitflag"])).all()
+    assert (H(a["inner_iters"]) == H(b["inner_iters"])).all()
+    assert np.max(np.abs(H(a["U"]) - H(b["U"]))) / cfg.umax <= 1e-12
+
+
 def _teacher_forced(ctl, N, mode, warm, k_sim=None, gen=None, **kw):
     """Each step, the GPU and the oracle get identical (x_k, rho, U_old); with
     warm=True the GPU also carries its active-set workspace from step to step
@@ -468,9 +534,21 @@ def test_step_matches_run_first_step(ctl):
 
 
 @pytest.mark.gpu
-def test_host_buffer_entry_points_match_device(ctl):
+@pytest.mark.parametrize("small_batch", [-1, 0])
+def test_host_buffer_entry_points_match_device(ctl, small_batch):
     """ntm_mpc_step / ntm_mpc_run with host arrays (the MEX boundary) give
-    bit-identical results to the device-pointer entry points."""
+    bit-identical results to the device-pointer entry points.  small_batch = 0
+    forces the far-workspace build, whose per-context HBM block the two entry
+    points share across streams (the context's own and the caller's): the
+    launches must be ordered on it, or the results drift run to run."""
+    ctl.set_small_batch(small_batch)
+    try:
+        _host_vs_device(ctl)
+    finally:
+        ctl.set_small_batch(-1)
+
+
+def _host_vs_device(ctl):
     N, B = 20, 40
     cfg, ocfg = cfgs(N, 2)
     x0 = np.ascontiguousarray(O.scenario_x0(np.arange(B)).T)
@@ -602,7 +680,8 @@ def test_full_size_batch_properties(ctl, N, mode):
         (the getWLc rows), to 1e-9 relative;
       * a seeded sample of 64 scenarios matches the oracle (teacher-forced);
       * batch-composition invariance: the same 64 scenarios run as their own
-        batch give bit-identical outputs (no cross-scenario coupling)."""
+        batch (on the same build) give bit-identical outputs (no cross-scenario
+        coupling)."""
     import ntm_mpc
     B = 100_000
     cfg, ocfg = cfgs(N, mode)
@@ -629,7 +708,13 @@ def test_full_size_batch_properties(ctl, N, mode):
     same = H(out["inner_iters"])[ids] == ref["inner_iters"]
     assert same.mean() >= 0.9
     assert np.max(np.abs(U[:, ids] - ref["U"])[:, same]) / cfg.umax <= (U_TOL_RATE if mode == 3 else U_TOL)
-    sub = ctl.step(T(xs), T(rs), T(us), cfg, active_ws=ws[:, ids].contiguous())
+    # the sub-batch takes the build the full batch took (the library picks the
+    # N = 20 build by batch size, ntm_ctx_set_small_batch; bit for bit holds within a build)
+    ctl.set_small_batch((1 << 62) if ctl.step_layout(B, cfg) == "lds" else 0)
+    try:
+        sub = ctl.step(T(xs), T(rs), T(us), cfg, active_ws=ws[:, ids].contiguous())
+    finally:
+        ctl.set_small_batch(-1)
     for k in ("U", "x_pred", "x_next", "exitflag", "inner_iters"):
         np.testing.assert_array_equal(H(sub[k]), H(out[k])[..., ids], err_msg=k)
 
