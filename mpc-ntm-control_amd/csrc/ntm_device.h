@@ -2226,6 +2226,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     int* const colrow = perm + (N + 1);                    // compact column -> row ending there
     bool sq = false;                                       // echelon path (k = nF - nS <= 1)
     int nc = -1;                                           // k = 1: the non-pivot compact column
+    int nc2 = -1;                                          // k = 1 with one collision: the second hole
     int xb = -1;                                           // one collision: the row left out of the triangle
     const int kdim = nF - nS;
     // Long horizons with rate rows (config 5) mostly give square sets with ONE
@@ -2260,15 +2261,21 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             nc = kdim ? uni<P>((int)__ffsll((long long)(holes >> (lane & ~(P - 1)))) - 1) : -1;
             if (l < nS) perm[l] = colrow[l + ((nc >= 0 && l >= nc) ? 1 : 0)];
             NTM_WSYNC();
-        } else if (kCollision && kdim == 0 && (int)__popcll(holes) == 1 &&
-                   (__ballot(l < nS && lastf < 0) & gmask) == 0) {
-            // one row does not own its last column (the column's owner is the last writer)
+        } else if (kCollision && (int)__popcll(holes) == kdim + 1 && (__ballot(l < nS && lastf < 0) & gmask) == 0) {
+            // one row does not own its last column (the column's owner is the last writer):
+            // k = 0 leaves one hole, k = 1 two (the triangle's spare column and the collision's)
             const unsigned long long orph = __ballot(l < nS && colrow[lastf < 0 ? 0 : lastf] != l) & gmask;
             if ((int)__popcll(orph) == 1) {
                 sq = true;
-                nc = uni<P>((int)__ffsll((long long)(holes >> (lane & ~(P - 1)))) - 1);
+                const unsigned long long hg = holes >> (lane & ~(P - 1));
+                nc = uni<P>((int)__ffsll((long long)hg) - 1);
+                if (kdim == 1) nc2 = uni<P>((int)__ffsll((long long)(hg & (hg - 1ull))) - 1);
                 xb = uni<P>((int)__ffsll((long long)(orph >> (lane & ~(P - 1)))) - 1);
-                if (l < nS - 1) perm[l] = colrow[l + (l >= nc ? 1 : 0)];
+                if (l < nS - 1) {
+                    int c = l + (l >= nc ? 1 : 0);
+                    if (nc2 >= 0 && c >= nc2) ++c;
+                    perm[l] = colrow[c];
+                }
                 NTM_WSYNC();
             }
         }
@@ -2366,7 +2373,11 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         // column pc(t) = t + (t >= nc); lower triangular, n x n row-major at Lp[t LD + u]),
         // the non-pivot column e_c (k = 1) and h
         const int n = nS - (xb >= 0 ? 1 : 0);
-        auto pc = [&](int u) { return u + ((nc >= 0 && u >= nc) ? 1 : 0); };
+        auto pc = [&](int u) {                                // pivot column of sorted row u
+            int c = u + ((nc >= 0 && u >= nc) ? 1 : 0);
+            if (kCollision && nc2 >= 0 && c >= nc2) ++c;
+            return c;
+        };
         double* const Ep = w.Ep();
         for (int idx = l; idx < n * n; idx += P) {
             const int t = idx / n, u = idx - t * n;
@@ -2376,10 +2387,11 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 Ep[w.eidx(t, u)] = (u <= t) ? gen_n(perm[t], w.fidx()[pc(u)]) : 0.0;
             }
         }
-        double acc = 0.0, acz = 0.0;
+        double acc = 0.0, acz = 0.0, acz2 = 0.0;
         if (l < n) {
             acc = hs_of(perm[l]);
             if (nc >= 0 && nc < pc(l)) acz = -gen_n(perm[l], w.fidx()[nc]);
+            if (kCollision && nc2 >= 0 && nc2 < pc(l)) acz2 = -gen_n(perm[l], w.fidx()[nc2]);
         }
         const double hxb = (kCollision && xb >= 0) ? hs_of(xb) : 0.0;   // before w.Phi() is reused
         NTM_WSYNC();
@@ -2387,7 +2399,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         NTM_ACC(ST_S_E, tp);
         // E_p V_p = h and (k = 1) E_p Z_p = -e_c: lane t owns row t; step t broadcasts
         // x_t (z_t) and updates the rows below
-        double x = 0.0, zz = 0.0;
+        double x = 0.0, zz = 0.0, zz2 = 0.0;
         double en = (l > 0 && l < n) ? Ep[w.eidx(l, 0)] : 0.0;   // E[l][t], loaded one step ahead
         for (int t = 0; t < n; ++t) {
             const double et = en;
@@ -2400,15 +2412,40 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 if (l == t) zz = zt;
                 acz -= et * zt;
             }
+            if (kCollision && nc2 >= 0) {
+                const double zt2 = gbcast<P>(acz2 * sq_id, t);
+                if (l == t) zz2 = zt2;
+                acz2 -= et * zt2;
+            }
         }
-        ok = gmaxi<P>((l < n && !(isfinite(x) && isfinite(zz))) ? 1 : 0) == 0;
-        // V_0 (pivots from E_p V_p = h, fixed values, 0 on the non-pivot column) and Z
-        const int rk = (fpos == nc) ? 0 : fpos - ((nc >= 0 && fpos > nc) ? 1 : 0);
+        ok = gmaxi<P>((l < n && !(isfinite(x) && isfinite(zz) && isfinite(zz2))) ? 1 : 0) == 0;
+        // V_0 (pivots from E_p V_p = h, fixed values, 0 on the non-pivot columns) and Z
+        const bool hole = fpos == nc || (kCollision && nc2 >= 0 && fpos == nc2);
+        const int rk = hole ? 0
+                            : fpos - ((nc >= 0 && fpos > nc) ? 1 : 0) - ((kCollision && nc2 >= 0 && fpos > nc2) ? 1 : 0);
         const double xs = __shfl(x, (l < N && !fixed) ? rk : 0, P);
         const double zs = __shfl(zz, (l < N && !fixed) ? rk : 0, P);
-        const double v0 = fixed ? vb : ((fpos == nc) ? 0.0 : xs);
+        const double v0 = fixed ? vb : (hole ? 0.0 : xs);
         vfin = v0;
-        if (kCollision && ok && xb >= 0) {
+        // k = 1 with one collision: V = V_0 + w1 Z1 + w2 Z2 (Zi = e_{hole i} + Zi_p); the row
+        // left out fixes a1 w1 + a2 w2 = h_B - n_B' V_0 (ai = n_B' Zi), which leaves the line
+        // V_p + w Z_d (eliminating the w with the larger |ai|) for the cost to minimise below
+        double vline = v0, zline = 0.0;
+        bool line = false;
+        if (kCollision && ok && xb >= 0 && nc2 >= 0) {
+            const double zs2 = __shfl(zz2, (l < N && !fixed) ? rk : 0, P);
+            const double z1 = fixed ? 0.0 : ((fpos == nc) ? 1.0 : (hole ? 0.0 : zs));
+            const double z2 = fixed ? 0.0 : ((fpos == nc2) ? 1.0 : (hole ? 0.0 : zs2));
+            const double nb = (l < N && !fixed) ? gen_n(xb, l) : 0.0;
+            const double b0 = gsum<P>(nb * v0), a1 = gsum<P>(nb * z1), a2 = gsum<P>(nb * z2);
+            const bool use2 = fabs(a2) >= fabs(a1);
+            const double ap = use2 ? a2 : a1, ao = use2 ? a1 : a2;
+            ok = ap != 0.0 && isfinite(ap) && isfinite(ao) && isfinite(b0);
+            const double zp = use2 ? z2 : z1, zo = use2 ? z1 : z2;
+            vline = ok ? v0 + ((hxb - b0) / ap) * zp : v0;
+            zline = ok ? zo - (ao / ap) * zp : 0.0;
+            line = ok;
+        } else if (kCollision && ok && xb >= 0) {
             // the row left out fixes the step along Z: n_B' (V_0 + w Z) = h_B
             const double zv = fixed ? 0.0 : ((fpos == nc) ? 1.0 : zs);
             const double nb = (l < N && !fixed) ? gen_n(xb, l) : 0.0;
@@ -2417,9 +2454,13 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             const double wv = ok ? (hxb - b0) / b1 : 0.0;
             vfin = v0 + wv * zv;
         } else if (ok && nc >= 0) {
+            zline = fixed ? 0.0 : ((fpos == nc) ? 1.0 : zs);
+            line = true;
+        }
+        if (line) {
             // k = 1: the minimum along V_0 + w Z, Z = e_c + Z_p:
             //   w = -(2 yz' Om (y0 + e - r)) / (2 yz' Om yz), y0 = Gamma D V_0, yz = Gamma D Z
-            const double zv = fixed ? 0.0 : ((fpos == nc) ? 1.0 : zs);
+            const double v0 = vline, zv = zline;
             if (l < N) {
                 w.U()[l] = w.D()[l] * v0;
                 w.d()[l] = w.D()[l] * zv;
@@ -2767,7 +2808,8 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             if (l < N && !fixed) w.d()[fpos] = res;
             NTM_WSYNC();
             const int n = nS - (xb >= 0 ? 1 : 0);
-            const int pl = l + ((nc >= 0 && l >= nc) ? 1 : 0);       // lane t's pivot column
+            int pl = l + ((nc >= 0 && l >= nc) ? 1 : 0);             // lane t's pivot column
+            if (kCollision && nc2 >= 0 && pl >= nc2) ++pl;
             double acc = (l < n) ? w.d()[pl] : 0.0, mu = 0.0;
             // one collision: a second right-hand side, the left-out row B at the pivot columns
             double acb = (kCollision && xb >= 0 && l < n) ? gen_n(xb, w.fidx()[pl]) : 0.0, mb = 0.0;
@@ -2783,11 +2825,18 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 }
             }
             if (kCollision && xb >= 0) {
-                // mu = a - mu_B b; the hole column's equation gives mu_B
+                // mu = a - mu_B b; a hole column's equation gives mu_B (with two holes,
+                // k = 1, the one with the larger pivot; the other holds at the optimum)
                 const double eh = (l < n && nc < pl) ? gen_n(perm[l], w.fidx()[nc]) : 0.0;
                 const double sa = gsum<P>(eh * mu), sb = gsum<P>(eh * mb);
-                const double den = gen_n(xb, w.fidx()[nc]) - sb;
-                const double muB = (w.d()[nc] - sa) / den;
+                double den = gen_n(xb, w.fidx()[nc]) - sb;
+                double muB = (w.d()[nc] - sa) / den;
+                if (nc2 >= 0) {
+                    const double eh2 = (l < n && nc2 < pl) ? gen_n(perm[l], w.fidx()[nc2]) : 0.0;
+                    const double sa2 = gsum<P>(eh2 * mu), sb2 = gsum<P>(eh2 * mb);
+                    const double den2 = gen_n(xb, w.fidx()[nc2]) - sb2;
+                    if (fabs(den2) > fabs(den)) { den = den2; muB = (w.d()[nc2] - sa2) / den2; }
+                }
                 mu -= muB * mb;
                 if (l == 0) w.np()[xb] = muB;
             }

@@ -719,36 +719,41 @@ def test_full_size_batch_properties(ctl, N, mode):
         np.testing.assert_array_equal(H(sub[k]), H(out[k])[..., ids], err_msg=k)
 
 
-def _one_collision(Lin, act, N):
-    """Does the active set have the long-horizon 'one collision' shape:
-    as many general rows as free variables, and exactly one free column in which
-    no general row ends (two rows end in the same one)?"""
+def _collision_kind(Lin, act, N):
+    """The long-horizon 'one collision' shapes: exactly one general row
+    does not own the last free column it ends in (another row ends there too),
+    with k = n_F - n_S = 0 (one free column where no row ends: kind 1) or k = 1
+    (two such columns: kind 2); 0 for any other set."""
     nz = [np.nonzero(np.abs(Lin[r]) > 0)[0] for r in act]
     fixed = {int(c[0]) for c in nz if len(c) == 1}
     free = [j for j in range(N) if j not in fixed]
     gen = [c for c in nz if len(c) > 1]
-    if len(gen) != len(free) or not gen:
-        return False
+    k = len(free) - len(gen)
+    if k not in (0, 1) or not gen:
+        return 0
     last = [max(j for j in c if j not in fixed) if any(j not in fixed for j in c) else -1 for c in gen]
     holes = [j for j in free if j not in last]
-    return len(holes) == 1 and -1 not in last
+    if -1 in last or len(holes) != k + 1 or len(set(last)) != len(gen) - 1:
+        return 0
+    return 1 + k
 
 
 def test_long_horizon_sets_vs_exact_kkt(ctl):
     """the N=50 re-solve paths (echelon k = 0 / 1, the one-collision
-    echelon set of config 5, the bordered elimination) checked against an exact
+    echelon sets of config 5 with k = 0 and k = 1, the bordered elimination) checked against an exact
     (30-digit) KKT solve of the SAME active set the device certified.  One QP per
     launch (i_sim = 1) so the QP's data are the launch inputs; the device's
     active set is read back from its warm-start workspace.  The exact solve must
     certify the set (primal feasible, multipliers >= 0) and the device's U must
-    match it to 1e-10 * umax; at least one set must be a one-collision set."""
-    N, B, steps = 50, 8, 4
+    match it to 1e-10 * umax; at least one set of each one-collision kind must be among them."""
+    N, B, steps = 50, 16, 6
     cfg, ocfg = cfgs(N, 3, i_sim=1)
     ph = O.Physics()
     x = O.scenario_x0(np.arange(B)).T
     rho, Uo = cbind.initial_state(x, ocfg)
     ws = ctl.new_active_ws(B, cfg)
-    n_coll = n_checked = 0
+    n_coll = [0, 0, 0]
+    n_checked = 0
     worst = 0.0
     for k in range(steps):
         tr, tu = T(rho), T(Uo)
@@ -763,15 +768,17 @@ def test_long_horizon_sets_vs_exact_kkt(ctl):
             Phi, Gam, Lam = O.lift(Rho, ph, ocfg)
             G, F = O.cost(Phi, Gam, Lam, x[:, s], ocfg)
             Lin, b = O.constraints(Phi, Gam, Lam, x[:, s], ocfg)
-            if k >= 2 and n_checked >= 12 and not _one_collision(Lin, act, N):
+            kind = _collision_kind(Lin, act, N)
+            if k >= 2 and n_checked >= 12 and (kind == 0 or (kind == 1 and n_coll[1] >= 6)):
                 continue                                    # keep the mpmath work bounded
             Ue, lam, cert = O.kkt_polish(G, F, Lin, b, act, dps=30)
             assert cert["max_violation"] <= 1e-9, (k, s, cert)
             assert cert["min_multiplier"] >= -1e-9 * max(1.0, np.max(np.abs(lam))), (k, s, cert)
             worst = max(worst, np.max(np.abs(U[:, s] - Ue)) / cfg.umax)
             n_checked += 1
-            n_coll += _one_collision(Lin, act, N)
+            n_coll[kind] += 1
         x, rho, Uo = H(out["x_next"]), H(tr), H(tu)         # the device's own closed loop
-    print(f"N=50 mode 3: {n_checked} sets checked, {n_coll} one-collision, max |U - U_exact| / umax = {worst:.2e}")
-    assert n_checked >= 8 and n_coll >= 1
+    print(f"N=50 mode 3: {n_checked} sets checked, {n_coll[1]} one-collision (k = 0), {n_coll[2]} one-collision "
+          f"(k = 1), max |U - U_exact| / umax = {worst:.2e}")
+    assert n_checked >= 8 and n_coll[1] >= 1 and n_coll[2] >= 1, n_coll
     assert worst <= 1e-10, worst
