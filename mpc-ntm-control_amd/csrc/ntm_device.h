@@ -185,7 +185,10 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        ST_K_Y, ST_K_CHK, ST_K_GRAD, ST_K_MU, ST_K_SUB, ST_C_A, ST_C_B, ST_C_Y, ST_C_SQ,
        ST_SC_COL, ST_SC_ROW, ST_SC_END, ST_L_COEF, ST_L_LOOP, CN_CYC_HIT, CN_CYC_SKIP };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
-constexpr int kMaxNT = 32;         // explicit R^{-1} in GI up to this horizon (WS::useT)
+#ifndef NTM_MAX_NT
+#define NTM_MAX_NT 32
+#endif
+constexpr int kMaxNT = NTM_MAX_NT; // explicit R^{-1} in GI up to this horizon (WS::useT)
 constexpr int kRepairs = 8;   // also at N = 50: 16 / 32 were no faster in mode 2, 6% / 10% slower in mode 3
 // A constant row (Lin_i = 0: the x_0 rows of getWLc, state rows Gamma doesn't
 // reach) is violated when b_i < -kConstTol (D22, oracle CONST_ROW_TOL): the same
@@ -433,8 +436,11 @@ struct WS {
     __device__ __forceinline__ int oJ() const { return 14 * n() + n() * (n() + 1); }
     __device__ __forceinline__ int oR() const { return oJ() + n() * ldj(); }
     // T = R^{-1} is kept for N <= kMaxNT only: at long horizons its N^2 doubles would
-    // halve the scenarios per CU, and the dual direction falls back to back substitution
-    __device__ __forceinline__ bool useT() const { return n() <= kMaxNT; }
+    // halve the scenarios per CU, and the dual direction falls back to back substitution.
+    // The far layouts keep no T either: maintaining it in HBM (a column per add, a
+    // Givens sweep and a row shift per drop) cost more than the back substitution
+    // on R saves (N = 20, 3 waves per SIMD: 10.09 -> 9.99 ms per step-batch without it)
+    __device__ __forceinline__ bool useT() const { return !kFar && n() <= kMaxNT; }
     __device__ __forceinline__ int oT() const { return oR() + (n() + 1) * ldj(); }
     // kFar: the E block (packed lower-triangular E, then 2(N+1) ints) replaces J/R/T in LDS
     __device__ __forceinline__ int oV() const {
@@ -465,7 +471,7 @@ struct WS {
     // T = R^{-1} of the GI factorisation (upper triangular, row-major n() x ldj();
     // zero outside the leading q x q block), so the dual direction is a matvec
     __device__ __forceinline__ double* T() const {
-        if constexpr (kFar) return far + (2 * n() + 1) * ldj();
+        if constexpr (kFar) return far;   // never dereferenced: far layouts keep no T (useT)
         else return base + oT();
     }
     // element (r, c) of J (and of T) at J()[r jr() + c jc()]: row-major in LDS,
@@ -534,12 +540,11 @@ struct WS {
 };
 
 __host__ __device__ inline int ldj_of(int N) { return N | 1; }
-// the J/R(/T) block: in LDS, or in HBM per scenario (far)
-__host__ __device__ inline int far_doubles(int N) {
-    return (N <= kMaxNT ? 2 : 1) * N * ldj_of(N) + (N + 1) * ldj_of(N);
-}
+// the J/R block of a far layout, in HBM per scenario (no T: WS::useT)
+__host__ __device__ inline int far_doubles(int N) { return N * ldj_of(N) + (N + 1) * ldj_of(N); }
 __host__ __device__ inline int ws_doubles(int N, bool far = false) {
-    const int jr = far ? (N * (N + 1)) / 2 + (N + 1) : far_doubles(N);
+    // LDS: the E block (far), or J, R and (N <= kMaxNT) T
+    const int jr = far ? (N * (N + 1)) / 2 + (N + 1) : (N <= kMaxNT ? 2 : 1) * N * ldj_of(N) + (N + 1) * ldj_of(N);
     return 14 * N + N * (N + 1) + jr + 24 * N + 6;
 }
 // workspace bytes with room for `rows` active-row flags: the structured rows of
