@@ -5,7 +5,9 @@
 //   CH = 4: 119.9 / 273.3   CH = 8: 120.3 / 276.5   CH = 10: 109.0 / 260.2
 //   CH = 16: 126.6 / 282.4  CH = 25: 119.6 / 271.8
 // 10 divides 50 (no masked tail chunk) and 5 chunks per horizon loop unroll
-// without spilling.
+// without spilling.  Re-measured on the round-3 build (far workspace, MFMA Gram,
+// B = 1e5, mode 2 / mode 3): CH = 10 140.4 / 297.3, CH = 25 141.0 / 299.2,
+// CH = 5 149.0 / 309.8, CH = 10 unrolled twice 147.2 / 306.8, CH = 5 twice 152.0 / 317.7.
 #ifdef NTM_N50_UNROLL
 #define NTM_CHUNK_UNROLL NTM_N50_UNROLL
 #endif
