@@ -238,15 +238,10 @@ def _verify_gathered(ctl, cfg, B_total, K, W, g, n_verify, seed=12345):
     x0 = np.concatenate([ntm_mpc.scenarios_x0(int(i), 1) for i in ids], axis=1)
     x = ctl.tensor(x0)
     n = len(ids)
-    # the recompute takes the build the gathered run took (the library picks the
-    # N = 20 build by batch size; bitwise equality holds within one build)
-    ctl.set_small_batch(1 << 62 if ctl.step_layout(B_total // int(os.environ.get("WORLD_SIZE", "1")), cfg) == "lds"
-                        else 0)
-    try:
-        leg = _run_leg(ctl, cfg, n, K, W, x, 0, 1, collect=True)
-        _finish_leg(ctl, leg, K)
-    finally:
-        ctl.set_small_batch(-1)
+    # the context is pinned to the build the whole batch takes on one GPU
+    # (dist.pin_layout in main), so the recompute runs the build the ranks ran
+    leg = _run_leg(ctl, cfg, n, K, W, x, 0, 1, collect=True)
+    _finish_leg(ctl, leg, K)
     sel = torch.as_tensor(ids, device=leg["hist"]["uk"].device)
     bad = [k for k, v in leg["hist"].items() if not bool((v == g[k].index_select(-1, sel)).all().item())]
     return {"scenarios": n, "ids_seed": seed, "bitwise_equal": not bad, "mismatched": bad}
@@ -273,12 +268,16 @@ def main():
     import ntm_mpc
     from ntm_mpc import Config, NtmMpc, ScenarioGen
     from ntm_mpc import flops as FL
-    from ntm_mpc.dist import gather_to_root
+    from ntm_mpc.dist import gather_to_root, pin_layout
 
     B, N, K, W = args.batch, args.N, args.steps, args.warmup
     cfg = Config(N=N, mode=args.mode)
     ctl = NtmMpc(config=cfg, device=local)
-    ctl.set_small_batch(args.small_batch)
+    if args.small_batch < 0:
+        # every rank, and rank 0's recompute, on the build one GPU takes for the whole batch
+        pin_layout(ctl, world * B, cfg)
+    else:
+        ctl.set_small_batch(args.small_batch)
     # shard: global scenario ids [rank*B, (rank+1)*B)  (shard-invariant inputs)
     x0 = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(rank * B, B), local)
 

@@ -113,6 +113,12 @@ int ntm_ctx_set_small_batch(ntm_ctx* ctx, int64_t max_scenarios);
 /* Which build a step/run launch of B scenarios at horizon N takes on this
  * context: *far = 1 for the far-workspace build, 0 for an all-LDS one. */
 int ntm_ctx_step_layout(const ntm_ctx* ctx, int32_t N, int64_t B, int32_t* far);
+/* The same for a full config, as the step/run launch of B scenarios would take it
+ * (flags included: the literal D4/D6 switches run on the generic kernels) and
+ * the launch shape of that kernel: lanes per scenario and the compile-time
+ * horizon (0 = generic).  ntm_ctx_step_layout is this with the default config. */
+int ntm_ctx_step_layout_cfg(const ntm_ctx* ctx, const ntm_config* cfg, int64_t B, int32_t* far, int32_t* lanes,
+                            int32_t* horizon_template);
 /* Diagnostic builds only: per-phase s_memtime cycle totals (48 counters);
  * NTM_E_UNSUPPORTED in production builds. */
 int ntm_debug_stamps(unsigned long long* out32, int reset);

@@ -49,9 +49,11 @@ switch mode
         [Rho, Uold] = ntm_mpc_mex('init', x0, cfg);   % Rho = repmat(rho(x0),1,N), Uold = +Inf
         WS = -ones(2 * (N + 1), B, 'int32');         % warm-start workspace, carried step to step
         X = x0;
+        k0_base = 0;                                 % the caller's first time index, as 'run' uses it
+        if ~isempty(gen) && isfield(gen, 'k0'), k0_base = gen.k0; end
         for k = 1:k_sim
             if ~isempty(gen)                         % the plant step's time index
-                gen.k0 = k - 1; ntm_mpc_mex('scenarios', gen);
+                gen.k0 = k0_base + k - 1; ntm_mpc_mex('scenarios', gen);
             end
             [U, XP, Xn, fl, it, Rho, Uold, WS] = ntm_mpc_mex('step', X, Rho, Uold, cfg, WS);
             wpred(:, k, :) = reshape(XP(1:2:end, :), N + 1, 1, B);

@@ -539,10 +539,10 @@ struct WS {
     __device__ __forceinline__ unsigned char* aflag() const { return fx() + n(); }
 };
 
-__host__ __device__ inline int ldj_of(int N) { return N | 1; }
+__host__ __device__ constexpr int ldj_of(int N) { return N | 1; }
 // the J/R block of a far layout, in HBM per scenario (no T: WS::useT)
-__host__ __device__ inline int far_doubles(int N) { return N * ldj_of(N) + (N + 1) * ldj_of(N); }
-__host__ __device__ inline int ws_doubles(int N, bool far = false) {
+__host__ __device__ constexpr int far_doubles(int N) { return N * ldj_of(N) + (N + 1) * ldj_of(N); }
+__host__ __device__ constexpr int ws_doubles(int N, bool far = false) {
     // LDS: the E block (far), or J, R and (N <= kMaxNT) T
     const int jr = far ? (N * (N + 1)) / 2 + (N + 1) : (N <= kMaxNT ? 2 : 1) * N * ldj_of(N) + (N + 1) * ldj_of(N);
     return 14 * N + N * (N + 1) + jr + 24 * N + 6;
@@ -550,12 +550,12 @@ __host__ __device__ inline int ws_doubles(int N, bool far = false) {
 // workspace bytes with room for `rows` active-row flags: the structured rows of
 // the MPC step are at most 8N+2 (getWLc 6N+4 plus 2(N-1) rate rows); a dense
 // quadprog problem (k_qp) may carry more
-__host__ __device__ inline int ws_bytes_rows(int N, int rows, bool far = false) {
+__host__ __device__ constexpr int ws_bytes_rows(int N, int rows, bool far = false) {
     const int flags = rows > 8 * N + 4 ? rows : 8 * N + 4;
     int b = ws_doubles(N, far) * 8 + 6 * (N + 1) * 4 + N + flags;   // ..., fx (N), aflag
     return (b + 15) & ~15;
 }
-__host__ __device__ inline int ws_bytes(int N, bool far = false) { return ws_bytes_rows(N, 8 * N + 4, far); }
+__host__ __device__ constexpr int ws_bytes(int N, bool far = false) { return ws_bytes_rows(N, 8 * N + 4, far); }
 
 // s: the scenario's index in the launch (its far block, when the WS has one)
 template <int NN, bool GEN = false, bool FAR = ws_far(NN)>
@@ -2041,6 +2041,63 @@ __device__ __forceinline__ bool polish_phase(const Prob& pb, const W& w, const R
         }
     }
     ok = gmaxi<P>(ok ? 0 : 1) == 0;
+    if (ok && Gsave) {
+        // One step of fixed-precision iterative refinement on the KKT residual with
+        // the same factors.  The range-space solve goes through L = chol(G~_FF),
+        // which loses digits when G~_FF is nearly singular although the KKT system
+        // is well conditioned (input-rate rows holding the last inputs: up to
+        // ~1e-8 umax off the exact optimum); the residual of the well-conditioned
+        // system, solved again, restores them.  Correction (dV, dmu):
+        //   G~_FF dV - E' dmu = -r1,  r1 = G~V + F~ - E'mu (free variables)
+        //   E dV = -r2,               r2 = n_s'V - bc_s   (general rows)
+        if (l < N) w.V()[l] = vfin;
+        NTM_WSYNC();
+        double r1 = 0.0, r2 = 0.0;
+        if (l < N && !fixed) {
+            r1 = w.F()[l];
+            for (int j = 0; j < N; ++j) r1 += ((j <= l) ? Gsave[l + j * LD] : Gsave[j + l * LD]) * w.V()[j];
+            for (int s = 0; s < nS; ++s) {
+                const int rid = w.sidx()[s];
+                r1 -= w.np()[s] * (-((rows->lin(w, rid, l) * w.D()[l]) / rows->rnorm(w, rid)));
+            }
+        }
+        if (l < nS) {
+            const int rid = w.sidx()[l];
+            const double rn = rows->rnorm(w, rid);
+            double nv = 0.0;
+            for (int j = 0; j < N; ++j) nv += (-((rows->lin(w, rid, j) * w.D()[j]) / rn)) * w.V()[j];
+            r2 = nv + rows->bval(w, rid) / rn;
+        }
+        const double dwl = fwd_lanes<P>(w.R(), w.ldi(), N, 1, LD, r1, l);
+        double dt = -dwl;
+        if (nS > 0) {
+            if (l < N) w.d()[l] = dwl;
+            NTM_WSYNC();
+            double rhs = 0.0;
+            if (l < nS) {
+                rhs = -r2;
+                for (int i = 0; i < N; ++i) rhs += w.J()[i * LDJ + l] * w.d()[i];
+            }
+            const double* K = w.R() + LD;
+            const double t1 = fwd_lanes<P>(K, w.kdi(), nS, LD, 1, rhs, l);
+            const double dmu = bwd_lanes<P>(K, w.kdi(), nS, LD, 1, t1, l);
+            NTM_WSYNC();
+            if (l < nS) {
+                w.d()[l] = dmu;
+                w.np()[l] += dmu;
+            }
+            NTM_WSYNC();
+            if (l < N) {
+                double sY = 0.0;
+                for (int a = 0; a < nS; ++a) sY += w.J()[l * LDJ + a] * w.d()[a];
+                dt = sY - dwl;
+            }
+        }
+        const double dv = bwd_lanes<P>(w.R(), w.ldi(), N, 1, LD, dt, l);
+        const double vr = fixed ? vb : vfin + dv;
+        ok = gmaxi<P>((l < N && !isfinite(vr)) ? 1 : 0) == 0;
+        if (ok) vfin = vr;
+    }
     if (ok) {
         // ---- KKT certificate ----
         if (l < N) w.V()[l] = vfin;

@@ -548,6 +548,7 @@ int launch_step(ntm_ctx* ctx, Prob pb, int64_t B, const double* x_k, double* rho
     lds += NTM_LDS_PAD;
 #endif
     const bool gen = pb.g.phys_on || pb.g.dist_on;     // the generator's build only when it is used
+    if (static_lds<P, NN>()) lds = 0;                  // the workspace is the kernel's static LDS
     int rc = gen ? set_lds(ctx, k_mpc_step<P, NN, true>, lds) : set_lds(ctx, k_mpc_step<P, NN, false>, lds);
     if (rc) return rc;
     int64_t blocks = (B + G - 1) / G;
@@ -582,7 +583,7 @@ int launch_run(ntm_ctx* ctx, Prob pb, int64_t B, int k_sim, const double* x0, do
     } else
 #endif
     {
-    const size_t lds = (size_t)G * ws_bytes(pb.N, ws_far(NN));
+    const size_t lds = static_lds<P, NN>() ? 0 : (size_t)G * ws_bytes(pb.N, ws_far(NN));
     if (int rc = attach_far<NN>(ctx, pb, B, st)) return rc;
     int rc = set_lds(ctx, k_mpc_run<P, NN>, lds);
     if (rc) return rc;
@@ -600,7 +601,16 @@ bool force_generic() {
     static bool g = std::getenv("NTM_GENERIC") != nullptr;
     return g;
 }
-bool use_generic(int flags) { return force_generic() || (flags & kGenericOnlyFlags) != 0; }
+// The generic kernels also take N = 20 with input-rate rows (mode 3, an extension
+// no BASELINE config runs at N = 20): they compile the one-collision re-solve
+// paths (polish_compact kCollision), whose null-space solve stays accurate where
+// two general rows end in the same free column.  The bordered elimination the
+// N = 20 kernel would take there factors a nearly singular G~_FF (the last inputs
+// act almost alike) and sat up to ~1e-8 umax off the exact optimum; compiled into
+// the N = 20 kernel the paths cost mode 2 ~1% through register allocation.
+bool use_generic(const ntm_config* c) {
+    return force_generic() || (c->flags & kGenericOnlyFlags) != 0 || (c->N == 20 && c->mode == NTM_MODE_FULL_DU);
+}
 #ifdef NTM_RU_ONLY20
 // resource-usage check of the N=20 hot kernel alone (make ru20): every horizon
 // goes to it; the library built this way is not for use
@@ -757,11 +767,29 @@ int ntm_ctx_set_small_batch(ntm_ctx* ctx, int64_t max_scenarios) {
 
 int ntm_ctx_step_layout(const ntm_ctx* ctx, int32_t N, int64_t B, int32_t* far) {
     if (!ctx || !far || N < 1 || N > NTM_MAX_N || B < 0) return NTM_E_INVALID;
+    ntm_config c;
+    ntm_config_default(&c, N);
     int32_t lanes = 0, nn = 0;
-    (void)ntm_step_launch_info(N, &lanes, &nn);
-    *far = (lanes == 64 && nn == 20) ? (small_batch<20>(ctx, B) ? 0 : (ws_far(20) ? 1 : 0))
-           : (lanes == 64 && nn == 50) ? (ws_far(50) ? 1 : 0)
-                                       : 0;
+    return ntm_ctx_step_layout_cfg(ctx, &c, B, far, &lanes, &nn);
+}
+
+int ntm_ctx_step_layout_cfg(const ntm_ctx* ctx, const ntm_config* cfg, int64_t B, int32_t* far, int32_t* lanes,
+                            int32_t* horizon_template) {
+    if (!ctx || !cfg || !far || !lanes || !horizon_template || cfg->N < 1 || cfg->N > NTM_MAX_N || B < 0)
+        return NTM_E_INVALID;
+    // the same decisions launch_step makes: the dispatch (generic kernels for the
+    // literal D4/D6 flags), then the N = 20 build by batch size, which only the
+    // multi-TU library has (single-TU builds run the ws_far(20) layout throughout)
+#define INFO(P_, NN_) (*lanes = (P_), *horizon_template = (NN_), 0)
+    (void)NTM_DISPATCH_P(cfg->N, use_generic(cfg), INFO);
+#undef INFO
+    const bool n20 = *lanes == 64 && *horizon_template == 20;
+    const bool n50 = *lanes == 64 && *horizon_template == 50;
+#ifndef NTM_SINGLE_TU
+    *far = n20 ? (small_batch<20>(ctx, B) ? 0 : (ws_far(20) ? 1 : 0)) : (n50 && ws_far(50) ? 1 : 0);
+#else
+    *far = n20 ? (ws_far(20) ? 1 : 0) : (n50 && ws_far(50) ? 1 : 0);
+#endif
     return NTM_OK;
 }
 
@@ -816,7 +844,7 @@ int ntm_mpc_step_ws_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_conf
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define CALL(P, NN) \
     launch_step<P, NN>(ctx, pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, active_ws, st)
-    return NTM_DISPATCH_P(cfg->N, use_generic(cfg->flags), CALL);
+    return NTM_DISPATCH_P(cfg->N, use_generic(cfg), CALL);
 #undef CALL
 }
 
@@ -893,7 +921,7 @@ int ntm_mpc_run_device(ntm_ctx* ctx, const ntm_physics* phys, const ntm_config* 
     if (ctx->gen_on) attach_gen(ctx->gen, phys, cfg, pb);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define CALL(P, NN) launch_run<P, NN>(ctx, pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, st)
-    return NTM_DISPATCH_P(cfg->N, use_generic(cfg->flags), CALL);
+    return NTM_DISPATCH_P(cfg->N, use_generic(cfg), CALL);
 #undef CALL
 }
 

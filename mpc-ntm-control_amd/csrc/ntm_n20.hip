@@ -22,4 +22,9 @@
 #define NTM_CH NTM_N20_CH
 #include "ntm_step.h"
 
-NTM_DEFINE_LAYOUT_LAUNCHERS(n20, 20, true)
+// the far layout is what the host side attaches a far block for (ws_far(20)); the
+// all-LDS N = 20 kernel is ntm_n20near.hip, so this TU requires NTM_FAR_N20
+#if !NTM_FAR_N20
+#error "ntm_n20.hip is the far-workspace N = 20 build: NTM_FAR_N20=0 applies to single-TU builds only"
+#endif
+NTM_DEFINE_LAYOUT_LAUNCHERS(n20, 20, ntm::ws_far(20))

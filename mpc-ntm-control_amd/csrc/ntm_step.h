@@ -152,6 +152,17 @@ __device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x
 // 8 scenarios per CU (small_batch in ntm_kernels.hip)
 #define NTM_WAVES_PER_EU(NN, FAR) \
     ((NN) > 32 ? 1 : ((NN) == 20 && (FAR) ? NTM_N20_WAVES_PER_EU : NTM_HOT_WAVES_PER_EU))
+// Compile-time horizons with one scenario per wave keep their workspace in a
+// static __shared__ array (the launch passes no dynamic LDS): every workspace
+// address is then a constant the backend folds into the ds_read/ds_write offset
+// field, where the dynamic-LDS base is an opaque value, so the loop-invariant
+// addresses of the dynamic layout were held in VGPRs (and spilled) instead
+#ifndef NTM_STATIC_LDS
+#define NTM_STATIC_LDS 1
+#endif
+template <int P, int NN>
+__host__ __device__ constexpr bool static_lds() { return NTM_STATIC_LDS && P == 64 && NN > 0; }
+
 template <int P, int NN, bool GEN, bool FAR = ws_far(NN)>
 __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN, FAR)) void k_mpc_step(Prob pb, int64_t B, const double* __restrict__ x_k,
                                                  double* __restrict__ rho, double* __restrict__ U_old,
@@ -166,7 +177,12 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN, FAR)) void k_mpc_step(Prob
     NTM_STAMPS_INIT();
     NTM_TRACE_SET(s, g, l);
     if (s >= B) return;
-    auto w = ws_carve<NN, GEN, FAR>(smem + g * ws_bytes(N, FAR), N, &pb, s);
+    char* sbase = smem + g * ws_bytes(N, FAR);
+    if constexpr (static_lds<P, NN>()) {
+        __shared__ __attribute__((aligned(16))) char smem_s[ws_bytes(NN > 0 ? NN : 1, FAR)];
+        sbase = smem_s;
+    }
+    auto w = ws_carve<NN, GEN, FAR>(sbase, N, &pb, s);
 #ifdef NTM_POISON
     // debug build (make poison): the workspace starts as NTM_POISON-valued doubles, so
     // a read of LDS this launch never wrote shows up as a run-to-run difference
@@ -218,7 +234,12 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN, FAR)) void k_mpc_run(Prob 
     const int64_t s = xcd_swizzle(blockIdx.x, gridDim.x) * G + g;
     const int N = NN > 0 ? NN : pb.N;
     if (s >= B) return;
-    auto w = ws_carve<NN, true, FAR>(smem + g * ws_bytes(N, FAR), N, &pb, s);
+    char* sbase = smem + g * ws_bytes(N, FAR);
+    if constexpr (static_lds<P, NN>()) {
+        __shared__ __attribute__((aligned(16))) char smem_s[ws_bytes(NN > 0 ? NN : 1, FAR)];
+        sbase = smem_s;
+    }
+    auto w = ws_carve<NN, true, FAR>(sbase, N, &pb, s);
     double x0 = x0v[2 * s], x1 = x0v[2 * s + 1];
     if (l < 2) w.cand()[l * (N + 1) + N] = -1;
     scn_store(pb, w, pb.g.first_id + s, l);           // this scenario's plasma (generator)
@@ -270,6 +291,7 @@ hipError_t ntm_launch_step_v(const ntm::Prob& pb, int64_t B, const double* x_k, 
                              double* x_pred, double* x_next, int32_t* exitflag, int32_t* inner_iters,
                              int32_t* active_ws, size_t lds, hipStream_t st) {
     const bool gen = pb.g.phys_on || pb.g.dist_on;     // the generator's build only when it is used
+    if (static_lds<64, NN>()) lds = 0;                 // the workspace is the kernel's static LDS
     hipError_t e = gen ? ntm_lds_opt_in(k_mpc_step<64, NN, true, FAR>, lds)
                        : ntm_lds_opt_in(k_mpc_step<64, NN, false, FAR>, lds);
     if (e != hipSuccess) return e;
@@ -286,6 +308,7 @@ template <int NN, bool FAR>
 hipError_t ntm_launch_run_v(const ntm::Prob& pb, int64_t B, int k_sim, const double* x0, double* xk, double* uk,
                             double* Uk, double* wpred, int32_t* exitflag, int32_t* inner_iters, size_t lds,
                             hipStream_t st) {
+    if (static_lds<64, NN>()) lds = 0;                 // the workspace is the kernel's static LDS
     hipError_t e = ntm_lds_opt_in(k_mpc_run<64, NN, FAR>, lds);
     if (e != hipSuccess) return e;
     if (B <= 0) return hipSuccess;

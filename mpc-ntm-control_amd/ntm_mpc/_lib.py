@@ -64,6 +64,8 @@ EXPORTS = {
     "ntm_ctx_set_stats": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ntm_ctx_set_small_batch": (C.c_int, [C.c_void_p, C.c_int64]),
     "ntm_ctx_step_layout": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.POINTER(C.c_int32)]),
+    "ntm_ctx_step_layout_cfg": (C.c_int, [C.c_void_p, _CFG, C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                          C.POINTER(C.c_int32)]),
     "ntm_debug_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "ntm_step_launch_info": (C.c_int, [C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "ntm_mpc_init": (C.c_int, [C.c_void_p, _PHY, _CFG, C.c_int64, _DP, _DP, _DP]),

@@ -264,20 +264,22 @@ class NtmMpc:
         self._raise(self.lib.ntm_ctx_set_scenarios(self._ctx, None if gen is None else C.byref(gen.to_c())),
                     "ntm_ctx_set_scenarios")
 
+    def _layout(self, B: int, cfg: Config):
+        far, lanes, nn = C.c_int32(), C.c_int32(), C.c_int32()
+        self._raise(self.lib.ntm_ctx_step_layout_cfg(self._ctx, C.byref(cfg.to_c()), int(B), C.byref(far),
+                                                     C.byref(lanes), C.byref(nn)), "ntm_ctx_step_layout_cfg")
+        return ("far" if far.value else "lds"), lanes.value, nn.value
+
     def step_layout(self, B: int, cfg: Config | None = None) -> str:
-        """Workspace layout of the build a launch of B scenarios takes: "far"
-        (J/R in a per-scenario HBM block) or "lds" (ntm_ctx_step_layout)."""
-        cfg = cfg or self.config
-        far = C.c_int32()
-        self._raise(self.lib.ntm_ctx_step_layout(self._ctx, cfg.N, int(B), C.byref(far)), "ntm_ctx_step_layout")
-        return "far" if far.value else "lds"
+        """Workspace layout of the build a launch of B scenarios with ``cfg``
+        (flags included) takes: "far" (J/R in a per-scenario HBM block) or "lds"
+        (ntm_ctx_step_layout_cfg)."""
+        return self._layout(B, cfg or self.config)[0]
 
     def step_kernel_name(self, B: int, cfg: Config | None = None) -> str:
         """Name of the fused step kernel specialisation a launch uses (reporting)."""
-        cfg = cfg or self.config
-        lanes, nn = C.c_int32(), C.c_int32()
-        self._raise(self.lib.ntm_step_launch_info(cfg.N, C.byref(lanes), C.byref(nn)), "ntm_step_launch_info")
-        return f"k_mpc_step<P={lanes.value},NN={nn.value},{self.step_layout(B, cfg)}>"
+        layout, lanes, nn = self._layout(B, cfg or self.config)
+        return f"k_mpc_step<P={lanes},NN={nn},{layout}>"
 
     # ------------------------------------------------------------ hot path
     def initial_state(self, x0: torch.Tensor, cfg: Config | None = None):

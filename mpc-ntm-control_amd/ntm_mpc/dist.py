@@ -3,7 +3,10 @@
 Scenarios are independent, so a node runs one process per GPU, each owning a
 contiguous range of GLOBAL scenario ids; the inputs are generated from the
 global id (counter-based), so any sharding reproduces the single-GPU batch
-bit for bit.  The only collective is the gather of the per-step outputs at
+bit for bit, provided every rank runs the build one GPU would run for the
+whole batch (``pin_layout``: the library picks the N = 20 build by batch size,
+and the two builds agree to the parity tolerances, not bit for bit).  The only
+collective is the gather of the per-step outputs at
 the end of the batch (RCCL over xGMI with the "nccl" backend; gloo on CPU):
 ``gather_scenarios`` leaves the whole batch on every rank (all-gather),
 ``gather_to_root`` only on one rank (each rank's block crosses xGMI once, into
@@ -22,6 +25,20 @@ def shard_range(total: int, world: int, rank: int) -> tuple[int, int]:
     base, rem = divmod(total, world)
     first = rank * base + min(rank, rem)
     return first, base + (1 if rank < rem else 0)
+
+
+def pin_layout(ctl, total: int, cfg=None) -> str:
+    """Pin ``ctl`` (an ntm_mpc.NtmMpc) to the step build a single GPU would take
+    for the whole ``total``-scenario batch, and return it ("lds" or "far").
+
+    The library chooses the N = 20 build from each call's batch size
+    (ntm_ctx_set_small_batch; all-LDS up to 32 scenarios per CU, the far
+    workspace above), so without this a far-build total sharded over many GPUs
+    would run its shards on the all-LDS build and lose bitwise agreement with
+    the one-GPU run.  Horizons with one build are unaffected."""
+    layout = ctl.step_layout(int(total), cfg)
+    ctl.set_small_batch((1 << 62) if layout == "lds" else 0)
+    return layout
 
 
 def gather_scenarios(t: torch.Tensor, total: int, group=None) -> torch.Tensor:
@@ -49,8 +66,10 @@ def gather_scenarios(t: torch.Tensor, total: int, group=None) -> torch.Tensor:
 def gather_to_root(t: torch.Tensor, total: int, root: int = 0, group=None):
     """Gather a (..., B_rank) scenario-minor tensor into (..., total) on ``root``
     only (None on the other ranks); ranks may hold uneven shares (shard_range).
-    One ``dist.gather`` of each rank's scenario-major block (RCCL point-to-point
-    sends into the root over xGMI)."""
+    ``root`` is a rank of ``group`` (group-relative, like the shares), converted
+    to the global rank ``dist.gather`` expects.  One ``dist.gather`` of each
+    rank's scenario-major block (RCCL point-to-point sends into the root over
+    xGMI)."""
     world = dist.get_world_size(group)
     if world == 1:
         return t
@@ -62,7 +81,8 @@ def gather_to_root(t: torch.Tensor, total: int, root: int = 0, group=None):
     pad[..., :t.shape[-1]] = t
     flat = pad.reshape(-1, bmax).t().contiguous()                  # (bmax, E)
     bufs = [torch.empty_like(flat) for _ in range(world)] if rank == root else None
-    dist.gather(flat, gather_list=bufs, dst=root, group=group)
+    dst = root if group is None else dist.get_global_rank(group, root)
+    dist.gather(flat, gather_list=bufs, dst=dst, group=group)
     if rank != root:
         return None
     parts = [bufs[r][:shares[r]] for r in range(world)]

@@ -582,6 +582,113 @@ static int orc_polish(int n, int m, const double* Gs, const double* Fs, const do
     return 1;
 }
 
+/* Partial-pivoting Gaussian elimination of the dense n x n row-major A (long
+ * double, destroyed) with right-hand side x (overwritten by the solution);
+ * 0 when a pivot vanishes. */
+static int ge_solve_ld(int n, long double* A, long double* x) {
+    for (int k = 0; k < n; ++k) {
+        int p = k;
+        for (int i = k + 1; i < n; ++i) if (fabsl(A[i * n + k]) > fabsl(A[p * n + k])) p = i;
+        if (!(A[p * n + k] != 0.0L)) return 0;
+        if (p != k) {
+            for (int j = 0; j < n; ++j) { long double t = A[k * n + j]; A[k * n + j] = A[p * n + j]; A[p * n + j] = t; }
+            long double t = x[k]; x[k] = x[p]; x[p] = t;
+        }
+        for (int i = k + 1; i < n; ++i) {
+            const long double f = A[i * n + k] / A[k * n + k];
+            for (int j = k; j < n; ++j) A[i * n + j] -= f * A[k * n + j];
+            x[i] -= f * x[k];
+        }
+    }
+    for (int k = n - 1; k >= 0; --k) {
+        long double s = x[k];
+        for (int j = k + 1; j < n; ++j) s -= A[k * n + j] * x[j];
+        x[k] = s / A[k * n + k];
+    }
+    return 1;
+}
+
+/* Accurate value on the final active set (oracle/ntm_oracle.py accurate_resolve,
+ * DESIGN.md §3): the KKT system of the free variables,
+ *   [G~_FF  N_SF'; N_SF  0] [V_F; -mu] = [-(F~_F + G~_FB V_B); bc_S - N_SB V_B],
+ * formed from the fp64 data in long double (Jacobi-scaled variables, unit-norm
+ * rows) and solved by partial-pivoting elimination plus one refinement step.
+ * The fp64 Cholesky / Schur re-solve loses digits when G~_FF is nearly singular
+ * (input-rate rows: ~6e-9 umax) although the KKT system is well conditioned.
+ * Variables fixed by single-entry rows keep U_j = b_a / Lin_aj.  U is left
+ * unchanged when the system is singular. */
+static void orc_accurate(int n, int m, const double* G, const double* F, const double* Lin, const double* b,
+                         const int* act, int q, double* U) {
+    static __thread long double M[4 * NMAX * NMAX], M2[4 * NMAX * NMAX], Ns[NMAX * NMAX];
+    long double D[NMAX], Vb[NMAX], g[NMAX], rhs[2 * NMAX], sol[2 * NMAX], res[2 * NMAX];
+    double Ufix[NMAX];
+    unsigned char fixed[NMAX];
+    int S[NMAX + 1], nS = 0, fidx[NMAX], nF = 0;
+    if (q <= 0) return;
+    memset(fixed, 0, sizeof fixed);
+    for (int j = 0; j < n; ++j) {
+        const double gj = G[(size_t)j * n + j];
+        D[j] = (gj > 0.0) ? (long double)(1.0 / sqrt(gj)) : 1.0L;   /* the fp64 Jacobi factors */
+        Vb[j] = 0.0L;
+    }
+    for (int a = 0; a < q; ++a) {
+        int row = act[a], nzc = 0, jj = -1;
+        for (int j = 0; j < n; ++j) if (Lin[(size_t)j * m + row] != 0.0) { ++nzc; jj = j; }
+        if (nzc == 1) {
+            Ufix[jj] = b[row] / Lin[(size_t)jj * m + row];
+            fixed[jj] = 1;
+            Vb[jj] = (long double)Ufix[jj] / D[jj];
+        } else if (nzc > 1) {
+            S[nS++] = row;
+        }
+    }
+    for (int j = 0; j < n; ++j) if (!fixed[j]) fidx[nF++] = j;
+    if (nF == 0) { for (int j = 0; j < n; ++j) U[j] = Ufix[j]; return; }
+    const int nt = nF + nS;
+    for (int i = 0; i < n; ++i) {
+        long double s = (long double)F[i] * D[i];
+        for (int j = 0; j < n; ++j) if (fixed[j]) s += ((long double)G[(size_t)j * n + i] * D[i] * D[j]) * Vb[j];
+        g[i] = s;
+    }
+    for (int a = 0; a < nF; ++a) {
+        for (int c = 0; c < nF; ++c)
+            M[a * nt + c] = (long double)G[(size_t)fidx[c] * n + fidx[a]] * D[fidx[a]] * D[fidx[c]];
+        rhs[a] = -g[fidx[a]];
+    }
+    for (int k = 0; k < nS; ++k) {
+        long double s2 = 0.0L;
+        for (int j = 0; j < n; ++j) { const long double v = (long double)Lin[(size_t)j * m + S[k]] * D[j]; Ns[k * NMAX + j] = v; s2 += v * v; }
+        const long double rn = sqrtl(s2);
+        long double h = (long double)b[S[k]] / rn;
+        for (int j = 0; j < n; ++j) {
+            Ns[k * NMAX + j] /= rn;
+            if (fixed[j]) h -= Ns[k * NMAX + j] * Vb[j];
+        }
+        for (int a = 0; a < nF; ++a) {
+            M[(nF + k) * nt + a] = Ns[k * NMAX + fidx[a]];
+            M[a * nt + nF + k] = Ns[k * NMAX + fidx[a]];
+        }
+        for (int c = 0; c < nS; ++c) M[(nF + k) * nt + nF + c] = 0.0L;
+        rhs[nF + k] = h;
+    }
+    memcpy(M2, M, sizeof(long double) * (size_t)nt * nt);
+    for (int i = 0; i < nt; ++i) sol[i] = rhs[i];
+    if (!ge_solve_ld(nt, M2, sol)) return;
+    for (int i = 0; i < nt; ++i) {                          /* one refinement step */
+        long double s = rhs[i];
+        for (int j = 0; j < nt; ++j) s -= M[i * nt + j] * sol[j];
+        res[i] = s;
+    }
+    memcpy(M2, M, sizeof(long double) * (size_t)nt * nt);
+    if (ge_solve_ld(nt, M2, res))
+        for (int i = 0; i < nt; ++i) sol[i] += res[i];
+    double Uo[NMAX];
+    for (int j = 0; j < n; ++j) Uo[j] = fixed[j] ? Ufix[j] : 0.0;
+    for (int a = 0; a < nF; ++a) Uo[fidx[a]] = (double)(sol[a] * D[fidx[a]]);
+    for (int j = 0; j < n; ++j) if (!isfinite(Uo[j])) return;
+    for (int j = 0; j < n; ++j) U[j] = Uo[j];
+}
+
 /* quadprog stand-in: Jacobi variable scaling U = D V (diag(DGD) = 1) and
  * unit-norm constraint rows, then Goldfarb-Idnani on the scaled problem
  * (cond(G) ~1e9-1e11 drops to ~1e6; see oracle/ntm_oracle.py qp_solve). */
@@ -607,7 +714,10 @@ static int orc_qp(int n, int m, const double* G, const double* F, const double* 
     int act[NMAX + 1], q = 0;
     int flag = orc_gi(n, m, Gs, Fs, Ls, bs, V, iters_out, act, &q);
     for (int j = 0; j < n; ++j) U[j] = V[j] * D[j];
-    if (flag == NTM_EXIT_OPTIMAL && gi_polish) (void)orc_polish(n, m, Gs, Fs, Ls, bs, Lin, b, D, act, q, U);
+    if (flag == NTM_EXIT_OPTIMAL && gi_polish) {
+        (void)orc_polish(n, m, Gs, Fs, Ls, bs, Lin, b, D, act, q, U);
+        orc_accurate(n, m, G, F, Lin, b, act, q, U);
+    }
     return flag;
 }
 

@@ -618,6 +618,93 @@ def _polish_certify(Gs, Fs, Ns, bcs, act, Lin, Dv, S, fixed, Ufix, V, mu):
     return V, U, True
 
 
+def _ge_solve_ld(M, rhs):
+    """Gaussian elimination with partial pivoting in extended precision
+    (np.longdouble: the x87 80-bit format, 64-bit significand, on x86-64, the
+    same type as the C oracle's ``long double``).  None when a pivot vanishes."""
+    A = np.array(M, dtype=np.longdouble)
+    x = np.array(rhs, dtype=np.longdouble)
+    n = A.shape[0]
+    for k in range(n):
+        p = k + int(np.argmax(np.abs(A[k:, k])))
+        if not A[p, k] != 0:
+            return None
+        if p != k:
+            A[[k, p]] = A[[p, k]]
+            x[[k, p]] = x[[p, k]]
+        f = A[k + 1:, k] / A[k, k]
+        A[k + 1:, k:] -= f[:, None] * A[k, k:][None, :]
+        x[k + 1:] -= f * x[k]
+    for k in range(n - 1, -1, -1):
+        x[k] = (x[k] - A[k, k + 1:] @ x[k + 1:]) / A[k, k]
+    return x
+
+
+def accurate_resolve(G, F, Lin, b, act, U):
+    """Accurate equality-constrained re-solve on a final active set.
+
+    The fp64 re-solves (polish_active_set) factor G~_FF by Cholesky and form the
+    Schur complement, which loses digits when G~_FF is nearly singular although
+    the KKT system itself is well conditioned (with input-rate rows the last two
+    inputs act almost alike: cond(G) ~1e11, re-solve errors up to ~6e-9 umax while
+    a one-ulp perturbation of the data moves the exact optimum by ~1e-16 umax).
+    This solves the KKT system of the free variables directly,
+        [G~_FF  N_SF'] [V_F ]   [-(F~_F + G~_FB V_B)]
+        [N_SF   0    ] [-mu ] = [  bc_S - N_SB V_B  ]
+    (Jacobi-scaled variables, unit-norm rows, all formed from the fp64 data in
+    long double), by partial-pivoting elimination in long double plus one
+    refinement step.  Variables fixed by single-entry rows keep U_j = b_a / Lin_aj
+    exactly.  Returns U (fp64), or the given U if the system is singular."""
+    n = G.shape[0]
+    act = [int(a) for a in act]
+    if not act:
+        return U
+    LD = np.longdouble
+    Dv = jacobi_scale(G).astype(LD)
+    fixed = np.zeros(n, dtype=bool)
+    Ufix = np.zeros(n)
+    S = []
+    for a in act:
+        nz = np.flatnonzero(Lin[a])
+        if len(nz) == 1:
+            j = nz[0]
+            Ufix[j] = b[a] / Lin[a, j]
+            fixed[j] = True
+        elif len(nz) > 1:
+            S.append(a)
+    free = np.flatnonzero(~fixed)
+    nF, nS = len(free), len(S)
+    if nF == 0:
+        return np.where(fixed, Ufix, U)
+    Gs = G.astype(LD) * Dv[:, None] * Dv[None, :]
+    Vb = np.where(fixed, Ufix.astype(LD) / Dv, LD(0))
+    g = F.astype(LD) * Dv + Gs[:, fixed] @ Vb[fixed]
+    M = np.zeros((nF + nS, nF + nS), dtype=LD)
+    rhs = np.zeros(nF + nS, dtype=LD)
+    M[:nF, :nF] = Gs[np.ix_(free, free)]
+    rhs[:nF] = -g[free]
+    if nS:
+        Ls = Lin[S].astype(LD) * Dv[None, :]
+        rn = np.sqrt(np.sum(Ls * Ls, axis=1))
+        Ns = Ls / rn[:, None]
+        bs = b[S].astype(LD) / rn
+        M[nF:, :nF] = Ns[:, free]
+        M[:nF, nF:] = Ns[:, free].T
+        rhs[nF:] = bs - Ns[:, fixed] @ Vb[fixed]
+    sol = _ge_solve_ld(M, rhs)
+    if sol is None:
+        return U
+    res = rhs - M @ sol
+    corr = _ge_solve_ld(M, res)
+    if corr is not None:
+        sol = sol + corr
+    Uo = np.where(fixed, Ufix, 0.0)
+    Uo[free] = np.asarray(sol[:nF] * Dv[free], dtype=np.float64)
+    if not np.all(np.isfinite(Uo)):
+        return U
+    return Uo
+
+
 def jacobi_scale(G):
     """D = diag(1/sqrt(G_jj)) (1 where G_jj <= 0)."""
     dg = np.diag(G)
@@ -656,6 +743,8 @@ def qp_solve(G, F, Lin, b, polish=False):
         Vp, Up, ok = polish_active_set(Gs, Fs, Ns, bcs, act, Lin, b, Dv)
         if ok:
             U, polished = Up, True
+        # the value on the final active set, accurate to the fp64 data
+        U = accurate_resolve(G, F, Lin, b, act, U)
     lam = np.asarray(lam) / rn[act] if len(act) else np.asarray(lam)
     info = {"active": list(act), "iters": its, "multipliers": lam, "polished": polished}
     if flag == EXIT_OK and polish:

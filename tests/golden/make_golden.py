@@ -94,11 +94,48 @@ def qp_fixture(N, mode, n):
              U_exact=np.stack(Us), exitflag=np.asarray(flags))
 
 
+def qp_traj_fixture(N, mode, n_scen, steps, name=None, dps=50):
+    """QPs along closed-loop trajectories of the C oracle (NTM_MPC_Sim.m:93-131):
+    for every scenario and step, the QP of the first inner iteration (the data
+    built from the carried rho, :94-97) with its optimum certified at ``dps``
+    digits on the NumPy oracle's final active set.  Mode 0 (BASELINE config 1)
+    starts from the reference x0 (NTM_MPC_Sim.m:34) with omega perturbed per
+    scenario, where the unconstrained LQ is well posed."""
+    from oracle import cbind
+    ph = O.Physics()
+    cfg = O.Config(N=N, mode=mode)
+    if mode == O.MODE_NONE:
+        x = np.tile(O.REFERENCE_X0[:, None], (1, n_scen))
+        x[1] *= 1.0 + 1e-3 * np.arange(n_scen)
+    else:
+        x = O.scenario_x0(np.arange(n_scen)).T.copy()
+    rho, Uo = cbind.initial_state(x, cfg)
+    Gs, Fs, Ls, bs, Us, flags, ks = [], [], [], [], [], [], []
+    for k in range(steps):
+        for s in range(n_scen):
+            Rho = rho[:, s].reshape(N, 3).T
+            Phi, Gam, Lam = O.lift(Rho, ph, cfg)
+            G, F = O.cost(Phi, Gam, Lam, x[:, s], cfg)
+            Lin, b = O.constraints(Phi, Gam, Lam, x[:, s], cfg)
+            U, flag, info = O.qp_solve(G, F, Lin, b)
+            if flag != O.EXIT_OK:
+                continue
+            Ue, _, cert = O.kkt_polish(G, F, Lin, b, info["active"], dps=dps)
+            assert cert["max_violation"] <= 1e-12 and cert["min_multiplier"] >= -1e-12, cert
+            Gs.append(G), Fs.append(F), Ls.append(Lin), bs.append(b), Us.append(Ue), flags.append(flag)
+            ks.append(k)
+        ref = cbind.step(x, rho, Uo, cfg)
+        x, rho, Uo = ref["x_next"], ref["rho"], ref["U_old"]
+    np.savez(HERE / (name or f"qp_m{mode}_N{N}.npz"), G=np.stack(Gs), F=np.stack(Fs), Lin=np.stack(Ls),
+             b=np.stack(bs), U_exact=np.stack(Us), exitflag=np.asarray(flags), step=np.asarray(ks))
+    print(f"qp_m{mode}_N{N}: {len(Us)} certified QPs")
+
+
 GEN = O.ScenarioGen(seed=20241220, first_id=0, k0=0, sigma_w=1e-3, sigma_omega=0.0, jbs_spread=0.1,
                     wdep_spread=0.1)
 
 
-def main(which=("functions", "closed_loop", "qp", "literal", "gen")):
+def main(which=("functions", "closed_loop", "qp", "literal", "gen", "qp_long", "closed_loop_long")):
     if "literal" in which:
         for flags in (O.LITERAL_PHI_RIGHTMUL, O.LITERAL_GAMMA_INDEX,
                       O.LITERAL_PHI_RIGHTMUL | O.LITERAL_GAMMA_INDEX):
@@ -110,9 +147,6 @@ def main(which=("functions", "closed_loop", "qp", "literal", "gen")):
     if "functions" in which:
         for N in (3, 20):
             functions_fixture(N)
-    if "closed_loop" not in which and "qp" not in which:
-        print("fixtures written to", HERE)
-        return
     if "closed_loop" in which:
         closed_loop_fixture(10, O.MODE_NONE, [0], 20)          # BASELINE config 1
         closed_loop_fixture(3, O.MODE_FULL, [0, 1, 2, 3], 20)
@@ -124,8 +158,16 @@ def main(which=("functions", "closed_loop", "qp", "literal", "gen")):
         qp_fixture(20, O.MODE_FULL, 12)
         qp_fixture(20, O.MODE_BOX, 8)
         qp_fixture(20, O.MODE_FULL_DU, 8)
+    if "qp_long" in which:
+        # BASELINE config 5 (N = 50, modes 2 and 3) and config 1 (N = 10, unconstrained)
+        qp_traj_fixture(50, O.MODE_FULL, 4, 4)
+        qp_traj_fixture(50, O.MODE_FULL_DU, 4, 4)
+        qp_traj_fixture(10, O.MODE_NONE, 4, 4)
+        qp_traj_fixture(10, O.MODE_FULL, 4, 4)
+    if "closed_loop_long" in which:
+        closed_loop_fixture(50, O.MODE_FULL_DU, [0, 1], 4)     # config 5 shape
     print("fixtures written to", HERE)
 
 
 if __name__ == "__main__":
-    main(tuple(sys.argv[1:]) or ("functions", "closed_loop", "qp", "literal", "gen"))
+    main(tuple(sys.argv[1:]) or ("functions", "closed_loop", "qp", "literal", "gen", "qp_long", "closed_loop_long"))

@@ -187,3 +187,37 @@ def test_mex_matches_ctypes_path(mex, ctl):
     mex("close", nout=0)
     assert mex.lib.t_clear() in (0, 1)
     torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["closed_loop_m0_N10.npz", "closed_loop_m2_N20.npz", "closed_loop_m3_N20.npz",
+                                  "closed_loop_gen_m2_N20.npz"])
+def test_mex_run_vs_closed_loop_fixture(mex, ctl, name):
+    """NTM_MPC_Sim_gpu.m's 'run' call (ntm_mpc_mex('run', x0, k_sim, cfg), with
+    'scenarios' first for a generator fixture) against the committed oracle
+    fixture directly: uk, Uk, xk, wpred, exit flags (exact) at the free-running
+    closed-loop tolerance of tests/test_gpu_golden.py (1e-6)."""
+    import math
+    d = np.load(ROOT / "tests" / "golden" / name)
+    mode = int(name.split("_m")[1][0])
+    N = int(name.split("_N")[1].split(".")[0])
+    k_sim = int(d["k_sim"])
+    S = d["x0"].shape[0]
+    if "gen_seed" in d.files:
+        mex("scenarios", {"seed": float(d["gen_seed"]), "first_id": float(d["gen_first_id"]), "k0": float(d["gen_k0"]),
+                          "sigma_w": float(d["gen_sigma_w"]), "sigma_omega": float(d["gen_sigma_omega"]),
+                          "jbs_spread": float(d["gen_jbs_spread"]), "wdep_spread": float(d["gen_wdep_spread"])},
+            nout=0)
+    try:
+        xk, uk, Uk, wp, fl, its = mex("run", np.ascontiguousarray(d["x0"].T), float(k_sim),
+                                      {"N": float(N), "mode": float(mode)}, nout=6)
+    finally:
+        mex("scenarios", np.zeros((0, 0)), nout=0)
+    np.testing.assert_array_equal(fl.T, d["exitflag"])
+    tol, umax = 1e-6, 2e6
+    assert np.max(np.abs(uk.T - d["uk"])) <= tol * umax
+    assert np.max(np.abs(Uk.reshape(k_sim, N, S).transpose(2, 1, 0) - d["Uk"])) <= tol * umax
+    xs = np.array([0.15, 2000 * math.pi])[None, :, None]
+    assert np.max(np.abs(xk.reshape(k_sim + 1, 2, S).transpose(2, 1, 0) - d["xk"]) / xs) <= tol
+    assert np.max(np.abs(wp.reshape(k_sim, N + 1, S).transpose(2, 0, 1) - d["wpred"])) <= tol * 0.15
+    assert (its.T == d["inner_iters"]).mean() >= 0.9

@@ -65,10 +65,9 @@ def test_c_step_teacher_forced(N, mode):
                 # solvers, or 2-cycle instead: compare along the C oracle's path
                 pc = dataclasses.replace(c, i_sim=int(ref["inner_iters"][s]), epsilon=-1.0)
                 out = O.mpc_step(x[:, s], rho[:, s].reshape(N, 3).T, Uo[:, s], PH, pc)
-            # mode 3 (config 5 extension): with rate rows the active KKT systems are
-            # ill-conditioned (cond(G) ~ 1e11); both fp64 restatements sit within
-            # ~4e-9 umax of a 30-digit solve of the same active set
-            tol = 5e-8 if mode == 3 else 1e-10
+            # both restatements end every QP with the long-double KKT solve on the
+            # final active set, mode 3's rate rows included
+            tol = 1e-10
             assert np.max(np.abs(out["U"] - ref["U"][:, s])) <= tol * max(c.umax, np.max(np.abs(out["U"])))
             np.testing.assert_allclose(out["xnext"], ref["x_next"][:, s], rtol=1e-10, atol=1e-15)
         x, rho, Uo = ref["x_next"], ref["rho"], ref["U_old"]
