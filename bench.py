@@ -310,9 +310,10 @@ def main():
     value = world * B * K / elapsed
     flop_step = FL.per_step(N, args.mode, r["qps"], r["tries"], r["giruns"], r["Kgi"], r["qact"], r["sgen"])
     achieved = flop_step * B / (r["kern_ms"] * 1e-3) / 1e12
-    traffic = None
+    traffic, traffic_source = None, None
     # PMC-measured HBM bytes per launch of this workload (tools/traffic_run.py,
-    # separate FETCH_SIZE / WRITE_SIZE passes): the latest round's file that matches
+    # separate FETCH_SIZE / WRITE_SIZE passes under rocprofv3, which this run cannot
+    # take itself): the latest round's committed file that matches, named in the line
     for prof in sorted((ROOT / "profiles").glob("traffic_r*.json"), reverse=True):
         try:
             tj = json.loads(prof.read_text())
@@ -320,6 +321,11 @@ def main():
             continue
         if tj.get("B") == B and tj.get("N") == N and tj.get("mode", 2) == args.mode:
             traffic = tj.get("hbm_bytes_per_launch")
+            traffic_source = {"file": str(prof.relative_to(ROOT)), "round": prof.stem.split("_r")[-1],
+                              "measured_in_this_run": False,
+                              "build": tj.get("build") or tj.get("commit"),
+                              "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the same workload "
+                                      "(tools/traffic_run.py), not this process"}
             break
     res = {
         "metric": "MPC steps/sec (whole node) at horizon N=20, batch=1e5 scenarios",
@@ -342,7 +348,7 @@ def main():
                                   "wpred, exitflag, inner_iters"
                        + (" [gloo rehearsal: ranks share devices]" if rehearsal and world > 1 else "")},
         "roofline": {"bound": "valu-fp64", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic, "traffic_source": traffic_source,
                      "kernel": ctl.step_kernel_name(B, cfg), "kernel_avg_ms": r["kern_ms"],
                      "flop_per_step": flop_step,
                      "flop_counters": "solver counters of the K timed launches (ntm_ctx_set_stats on in the "

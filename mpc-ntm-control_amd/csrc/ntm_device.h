@@ -413,6 +413,9 @@ __device__ __forceinline__ double coef_b(const Coef& k, double r3) { return k.bc
 #ifndef NTM_FAR_N20
 #define NTM_FAR_N20 1
 #endif
+#ifndef NTM_OTHER_SLOT
+#define NTM_OTHER_SLOT 0     // 1: long horizons try this step's other certified set before GI (qp_phase); 2: every horizon
+#endif
 #ifndef NTM_FAR_JB
 #define NTM_FAR_JB 0         // columns per trip of the bordered elimination's loads in the far block (0: two, loaded as used)
 #endif
@@ -3155,7 +3158,11 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                 // written at even iterations); when its repairs fail, its
                 // receding-horizon shift is tried before GI (it hits in the
                 // transient of the first steps, where the plan moves in time)
-                bool alt = it == 2 && pb.mode != NTM_MODE_NONE;
+                // long horizons (NTM_OTHER_SLOT): before the shifted set, this step's
+                // other certified set (slot 0 at it = 2: iteration 1's) gets one try
+                // too before GI, whose N = 50 solves cost ~1-2M cycles each
+                constexpr bool kOther = NTM_OTHER_SLOT >= 2 || (NTM_OTHER_SLOT && (W::kNN > 32 || W::kNN == 0));
+                int alt = (it == 2 && pb.mode != NTM_MODE_NONE) ? (kOther ? 2 : 1) : 0;
                 int keep_id = -1, keep_q = -1;     // the repaired set (lane l: entry l) while the shift is tried
                 // certified re-solve of the candidate; on failure, up to kRepairs
                 // single-row repairs (add the most violated row and/or drop the row
@@ -3234,12 +3241,24 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                     }
                     if (stop) {
                         if (!alt) break;
-                        alt = false;                       // last try: the shifted carried set
-                        NTM_CNT(CN_ALT_TRY);
-                        keep_id = (l < cq) ? w.act()[l] : -1;
-                        keep_q = cq;
+                        if (keep_q < 0) {                  // the repaired set, for GI's warm start
+                            keep_id = (l < cq) ? w.act()[l] : -1;
+                            keep_q = cq;
+                        }
                         NTM_WSYNC();
-                        cq = shifted_into_act<P>(pb, w, cand, l);
+                        const int* other = w.cand() + (slot ^ 1) * (N + 1);
+                        const int oq = kOther ? uni<P>(other[N]) : -1;
+                        if (kOther && alt == 2 && oq >= 0) {   // this step's other certified set
+                            NTM_CNT(CN_ALT_TRY);
+                            if (l < oq) w.act()[l] = other[l];
+                            cq = oq;
+                            NTM_WSYNC();
+                            alt = 1;
+                        } else {                           // the shifted carried set
+                            NTM_CNT(CN_ALT_TRY);
+                            cq = shifted_into_act<P>(pb, w, cand, l);
+                            alt = 0;
+                        }
                         rep = -2;                          // counted as neither a first try nor a repair
                     }
                     NTM_WSYNC();

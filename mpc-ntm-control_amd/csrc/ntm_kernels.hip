@@ -616,11 +616,17 @@ bool use_generic(const ntm_config* c) {
 // goes to it; the library built this way is not for use
 #define NTM_DISPATCH_P(N, GEN, CALL) CALL(64, 20)
 #else
+#ifdef NTM_EXP_P32
+// experiment: N = 20 with two scenarios per wave on the far layout
+#define NTM_N20_CALL(CALL) CALL(32, 20)
+#else
+#define NTM_N20_CALL(CALL) CALL(64, 20)
+#endif
 #define NTM_DISPATCH_P(N, GEN, CALL)                                                \
     ((GEN) ? (lanes_for(N) == 16 ? CALL(16, 0) : (lanes_for(N) == 32 ? CALL(32, 0) : CALL(64, 0))) \
     : lanes_for(N) == 16 ? ((N) == 10 ? CALL(16, 10) : CALL(16, 0))                  \
                         : (lanes_for(N) == 32 ? CALL(32, 0)                          \
-                                              : ((N) == 20 ? CALL(64, 20)            \
+                                              : ((N) == 20 ? NTM_N20_CALL(CALL)      \
                                                            : ((N) == 50 ? CALL(64, 50) : CALL(64, 0)))))
 #endif
 

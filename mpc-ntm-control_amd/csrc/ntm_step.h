@@ -152,6 +152,9 @@ __device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x
 // 8 scenarios per CU (small_batch in ntm_kernels.hip)
 #define NTM_WAVES_PER_EU(NN, FAR) \
     ((NN) > 32 ? 1 : ((NN) == 20 && (FAR) ? NTM_N20_WAVES_PER_EU : NTM_HOT_WAVES_PER_EU))
+// two scenarios per wave at N = 20 (far layout, 24 KB of LDS per wave): at most 6
+// waves per CU fit, so the register budget of 2 waves per SIMD costs nothing
+#define NTM_WAVES_PER_EU_P(P, NN, FAR) ((P) < 64 && (NN) == 20 ? 2 : NTM_WAVES_PER_EU(NN, FAR))
 // Compile-time horizons with one scenario per wave keep their workspace in a
 // static __shared__ array (the launch passes no dynamic LDS): every workspace
 // address is then a constant the backend folds into the ds_read/ds_write offset
@@ -164,7 +167,7 @@ template <int P, int NN>
 __host__ __device__ constexpr bool static_lds() { return NTM_STATIC_LDS && P == 64 && NN > 0; }
 
 template <int P, int NN, bool GEN, bool FAR = ws_far(NN)>
-__global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN, FAR)) void k_mpc_step(Prob pb, int64_t B, const double* __restrict__ x_k,
+__global__ __launch_bounds__(64, NTM_WAVES_PER_EU_P(P, NN, FAR)) void k_mpc_step(Prob pb, int64_t B, const double* __restrict__ x_k,
                                                  double* __restrict__ rho, double* __restrict__ U_old,
                                                  double* __restrict__ U, double* __restrict__ x_pred,
                                                  double* __restrict__ x_next, int32_t* __restrict__ exitflag,
@@ -225,7 +228,7 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN, FAR)) void k_mpc_step(Prob
 }
 
 template <int P, int NN, bool FAR = ws_far(NN)>
-__global__ __launch_bounds__(64, NTM_WAVES_PER_EU(NN, FAR)) void k_mpc_run(Prob pb, int64_t B, int k_sim, const double* __restrict__ x0v,
+__global__ __launch_bounds__(64, NTM_WAVES_PER_EU_P(P, NN, FAR)) void k_mpc_run(Prob pb, int64_t B, int k_sim, const double* __restrict__ x0v,
                                                 double* xk, double* uk, double* Uk, double* wpred,
                                                 int32_t* exitflag, int32_t* inner_iters) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
