@@ -413,9 +413,6 @@ __device__ __forceinline__ double coef_b(const Coef& k, double r3) { return k.bc
 #ifndef NTM_FAR_N20
 #define NTM_FAR_N20 1
 #endif
-#ifndef NTM_OTHER_SLOT
-#define NTM_OTHER_SLOT 0     // 1: long horizons try this step's other certified set before GI (qp_phase); 2: every horizon
-#endif
 #ifndef NTM_FAR_JB
 #define NTM_FAR_JB 0         // columns per trip of the bordered elimination's loads in the far block (0: two, loaded as used)
 #endif
@@ -2838,8 +2835,22 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     }
     }
     NTM_ACC(ST_P_BWD, tp);
-    if (ok) {
+    // Generic kernels: one step of fixed-precision iterative refinement after the
+    // bordered elimination.  Its range-space factor goes through L L' = G~_FF, which
+    // loses digits when G~_FF is nearly singular although the KKT system is well
+    // conditioned (input-rate rows holding the last inputs, N = 20 mode 3, which
+    // runs here: ~1e-9 umax off the exact optimum).  Pass 0 of the certificate
+    // loop computes the KKT residual [r1; r2] (r1 = G~V + F~ - E'mu on the free
+    // variables, r2 = n_s'V - bc_s on the general rows), solves A [dV; -dmu] =
+    // -[r1; r2] with the same factor (forward and backward sweeps), and pass 1
+    // certifies the corrected point.  The specialised N = 20 / 50 kernels keep the
+    // single pass (their register allocation decides their speed).
+    constexpr bool kRefine = W::kNN == 0;
+    bool refine = kRefine && ok && !sq && fused;
+    double r2 = 0.0;
+    for (int pass = 0; ok; ++pass) {
         // ---- KKT certificate ----
+        const bool resid = refine && pass == 0;
         if (l < N) { w.V()[l] = vfin; w.U()[l] = w.D()[l] * vfin; }
         NTM_WSYNC();
         // y = Gamma U once, for the primal check (state rows) and the gradient
@@ -2848,9 +2859,25 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             NTM_WSYNC();
         }
         NTM_ACC(ST_K_Y, tp);
-        double vmax = gmax<P>(l < N ? fabs(vfin) : 0.0);
-        Pick vf = rows.template check<P>(w, vfin, l, true, fmax(1.0, vmax), w.xp());
-        ok = vf.p == 0;
+        Pick vf{};
+        if (resid) {
+            if (l < nS) {                                  // primal residual of general row l
+                const int r = w.srw()[l];
+                const double sg = w.ssg()[l];
+                if (r >= 2 * N) {
+                    const int i = r - 2 * N;
+                    r2 = w.idun()[i] * (rows.du - sg * (w.U()[i] - w.U()[i - 1]));
+                } else {
+                    const int c = r & 1;
+                    const double bval = (sg > 0.0) ? (rows.xmax(c) - w.e()[r]) : (-rows.xmin(c) + w.e()[r]);
+                    r2 = w.irn()[r] * (bval - sg * w.xp()[r]);
+                }
+            }
+        } else {
+            double vmax = gmax<P>(l < N ? fabs(vfin) : 0.0);
+            vf = rows.template check<P>(w, vfin, l, true, fmax(1.0, vmax), w.xp());
+            ok = vf.p == 0;
+        }
         NTM_ACC(ST_K_CHK, tp);
         // gradient G~V + F~ = D (2 Gamma' Om y) + F~
         // (y is dead after the primal check: Om y in place, once per stage)
@@ -2949,6 +2976,75 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                     if (w.srw()[s2] >= 2 * N) res -= w.np()[s2] * gen_n(s2, l);
         }
         NTM_ACC(ST_K_SUB, tp);
+        if constexpr (kRefine) {
+            if (resid) {
+                // right-hand side -[r1; r2] in bordered-row order (scratch: w.Phi(), dead
+                // after the sparse pass above), then L_A z = b, L_A' x = diag(I, -I) z
+                NTM_WSYNC();
+                if (l < N && !fixed) z[fpos] = -res;
+                if (l < nS) z[nF + l] = -r2;
+                NTM_WSYNC();
+                auto slot_of = [&](const double* v, int k) -> double {   // v[k / P] (k uniform)
+                    double o = v[0];
+#pragma unroll
+                    for (int r = 1; r < RPL; ++r) o = (k / P == r) ? v[r] : o;
+                    return o;
+                };
+                double acc[RPL], xr[RPL];
+#pragma unroll
+                for (int r = 0; r < RPL; ++r) {
+                    const int lr = l + r * P;
+                    acc[r] = (lr < nt) ? z[lr] : 0.0;
+                    xr[r] = 0.0;
+                }
+                for (int k = 0; k < nt; ++k) {             // forward: L_A z = b
+                    const double zk = gbcast<P>(slot_of(acc, k), k % P) * w.ldi()[k];
+#pragma unroll
+                    for (int r = 0; r < RPL; ++r) {
+                        const int lr = l + r * P;
+                        if (lr == k) xr[r] = zk;
+                        if (lr > k && lr < nt) acc[r] -= Lp[w.brow(lr) + w.bcol(k, nt)] * zk;
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < RPL; ++r) {
+                    const int lr = l + r * P;
+                    acc[r] = (lr < nF) ? xr[r] : -xr[r];
+                    xr[r] = 0.0;
+                }
+                for (int k = nt - 1; k >= 0; --k) {        // backward: L_A' x = diag(I, -I) z
+                    const double xk = gbcast<P>(slot_of(acc, k), k % P) * w.ldi()[k];
+#pragma unroll
+                    for (int r = 0; r < RPL; ++r) {
+                        const int lr = l + r * P;
+                        if (lr == k) xr[r] = xk;
+                        if (lr < k) acc[r] -= Lp[w.brow(k) + w.bcol(lr, nt)] * xk;
+                    }
+                }
+                // x = [dV_F; -dmu]: V_F in rows < nF <= N <= P (slot 0)
+                const double dvs = __shfl(xr[0], (l < N && !fixed) ? fpos : 0, P);
+                const double vr = fixed ? vfin : vfin + dvs;
+                bool good = !(l < N) || isfinite(vr);
+                NTM_WSYNC();
+#pragma unroll
+                for (int r = 0; r < RPL; ++r) {
+                    const int lr = l + r * P;
+                    if (lr >= nF && lr < nt) good = good && isfinite(w.np()[lr - nF] - xr[r]);
+                }
+                good = gmaxi<P>(good ? 0 : 1) == 0;
+                if (good) {
+                    vfin = vr;
+#pragma unroll
+                    for (int r = 0; r < RPL; ++r) {
+                        const int lr = l + r * P;
+                        if (lr >= nF && lr < nt) w.np()[lr - nF] -= xr[r];
+                    }
+                }
+                NTM_WSYNC();
+                refine = false;
+                continue;
+            }
+        }
         // multipliers: general row s on lane s, fixed variable j on lane j; each
         // lane keeps its most negative one and that row's active-list position
         double mval = 0.0;
@@ -2969,6 +3065,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         fk = !ok ? (dual_ok ? 2 : 4) : (!dual_ok ? 1 : 0);
         fpos_out = mpos;
         ok = ok && dual_ok;
+        break;
     }
     ok = gmaxi<P>(ok ? 0 : 1) == 0;
     NTM_ACC(ST_P_KKT, tp);
@@ -3152,17 +3249,24 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
             if (cq0 >= 0) {
                 NTM_CNT(CN_CAND);
                 int cq = cq0;
-                if (l < cq) w.act()[l] = cand[l];
-                NTM_WSYNC();
+                // long horizons shift the carried set first at iteration 2: offline
+                // (NumPy oracle, steps 5-12) the receding-horizon shift of the previous
+                // step's last even set is iteration 2's optimum for 75% of the N = 50
+                // scenario-steps (mode 2; 72% in mode 3) and the unshifted set for 19%;
+                // at N = 20 the unshifted set wins (55% against 18%)
+                const bool shift_first = (W::kNN > 32 || (W::kNN == 0 && N > 32)) && it == 2 &&
+                                         pb.mode != NTM_MODE_NONE;
+                if (shift_first) {
+                    cq = shifted_into_act<P>(pb, w, cand, l);
+                } else {
+                    if (l < cq) w.act()[l] = cand[l];
+                    NTM_WSYNC();
+                }
                 // iteration 2: the carried set is the previous step's (slot 1 is only
                 // written at even iterations); when its repairs fail, its
                 // receding-horizon shift is tried before GI (it hits in the
                 // transient of the first steps, where the plan moves in time)
-                // long horizons (NTM_OTHER_SLOT): before the shifted set, this step's
-                // other certified set (slot 0 at it = 2: iteration 1's) gets one try
-                // too before GI, whose N = 50 solves cost ~1-2M cycles each
-                constexpr bool kOther = NTM_OTHER_SLOT >= 2 || (NTM_OTHER_SLOT && (W::kNN > 32 || W::kNN == 0));
-                int alt = (it == 2 && pb.mode != NTM_MODE_NONE) ? (kOther ? 2 : 1) : 0;
+                bool alt = it == 2 && pb.mode != NTM_MODE_NONE;
                 int keep_id = -1, keep_q = -1;     // the repaired set (lane l: entry l) while the shift is tried
                 // certified re-solve of the candidate; on failure, up to kRepairs
                 // single-row repairs (add the most violated row and/or drop the row
@@ -3241,23 +3345,17 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                     }
                     if (stop) {
                         if (!alt) break;
-                        if (keep_q < 0) {                  // the repaired set, for GI's warm start
-                            keep_id = (l < cq) ? w.act()[l] : -1;
-                            keep_q = cq;
-                        }
+                        alt = false;                       // last try: the other form of the carried set
+                        NTM_CNT(CN_ALT_TRY);
+                        keep_id = (l < cq) ? w.act()[l] : -1;   // the repaired set, for GI's warm start
+                        keep_q = cq;
                         NTM_WSYNC();
-                        const int* other = w.cand() + (slot ^ 1) * (N + 1);
-                        const int oq = kOther ? uni<P>(other[N]) : -1;
-                        if (kOther && alt == 2 && oq >= 0) {   // this step's other certified set
-                            NTM_CNT(CN_ALT_TRY);
-                            if (l < oq) w.act()[l] = other[l];
-                            cq = oq;
+                        if (shift_first) {                 // the unshifted carried set
+                            cq = cq0;
+                            if (l < cq) w.act()[l] = cand[l];
                             NTM_WSYNC();
-                            alt = 1;
                         } else {                           // the shifted carried set
-                            NTM_CNT(CN_ALT_TRY);
                             cq = shifted_into_act<P>(pb, w, cand, l);
-                            alt = 0;
                         }
                         rep = -2;                          // counted as neither a first try nor a repair
                     }

@@ -32,6 +32,12 @@ U_TOL = 1e-10
 U_TOL_RATE = 1e-10
 # predicted / next states, relative to |w| ~ 0.15 m and |omega| ~ 2000 pi: 1e-9
 X_TOL, X_TOL_RATE = 1e-9, 1e-9
+# free-running closed loops against the C oracle over 20 steps: the loop feeds each
+# step's rounding back through rho(x) (per-step errors of ~1e-12 umax grow to
+# ~1e-9 by step 20: measured 1.2e-9 to 3.3e-9 in modes 1-3, N = 20 and 50), so the
+# bound is 1e-8, 100x tighter than round 3's 1e-6 (whose oracle sat ~1e-9 off the
+# exact optimum itself)
+RUN_TOL = 1e-8
 
 
 def T(a):
@@ -227,7 +233,7 @@ def test_run_closed_loop_far_build(ctl, mode):
         out = ctl.run(T(x0), k_sim, cfg)
     finally:
         ctl.set_small_batch(-1)
-    _assert_run_close(out, ref, cfg, k_sim)
+    _assert_run_close(out, ref, cfg, k_sim, tol=RUN_TOL, x0=x0, ocfg=ocfg)
 
 
 def test_step_layout_by_batch(ctl):
@@ -523,7 +529,7 @@ def test_step_ragged_batches(ctl, B):
 
 
 # ---------------------------------------------------------------- closed loop
-@pytest.mark.parametrize("N,mode", [(10, 0), (20, 1), (20, 2), (20, 3)])
+@pytest.mark.parametrize("N,mode", [(10, 0), (20, 1), (20, 2), (20, 3), (50, 2), (50, 3)])
 def test_run_closed_loop(ctl, N, mode):
     """ntm_mpc_run (NTM_MPC_Sim.m:80-131) against the C oracle's closed loop: every
     workspace output north_star names, the applied inputs uk, the plans Uk
@@ -534,21 +540,66 @@ def test_run_closed_loop(ctl, N, mode):
     x0 = O.scenario_x0(np.arange(B)).T if mode else np.tile(O.REFERENCE_X0[:, None], (1, B))
     ref = cbind.run(x0, ocfg, k_sim)
     out = ctl.run(T(x0), k_sim, cfg)
-    _assert_run_close(out, ref, cfg, k_sim)
+    # mode 0: the unconstrained minimisers reach ~1e11 (reference x0), so 1e-10 of
+    # umax would ask for 1e-15 relative; the round-3 1e-6 stays
+    _assert_run_close(out, ref, cfg, k_sim, tol=RUN_TOL if mode else 1e-6, x0=x0, ocfg=ocfg)
 
 
-def _assert_run_close(out, ref, cfg, k_sim, tol=1e-6):
+def _replay_along(x0s, ocfg, iters, gen, sid):
+    """The C oracle's closed loop for one scenario (global id ``sid`` of ``gen``)
+    along a given path: step k runs exactly iters[k] LPV iterations (no early
+    stop), so a scenario whose bitwise stopping rule (NTM_MPC_Sim.m:123-125)
+    fired at another iteration on the GPU is checked on the GPU's own path.
+    Returns the histories in ntm_mpc_run's layout (one column)."""
+    N, K = ocfg.N, len(iters)
+    g0 = None if gen is None else dataclasses.replace(gen, first_id=gen.first_id + sid)
+    x = np.ascontiguousarray(x0s.reshape(2, 1))
+    if g0 is None:
+        rho, Uo = cbind.initial_state(x, ocfg)
+    else:
+        rho, Uo = cbind.initial_state_gen(x, ocfg, g0)
+    h = {"xk": np.zeros((2 * (K + 1), 1)), "uk": np.zeros((K, 1)), "Uk": np.zeros((N * K, 1)),
+         "wpred": np.zeros(((N + 1) * K, 1)), "exitflag": np.zeros((K, 1), np.int32),
+         "inner_iters": np.zeros((K, 1), np.int32)}
+    h["xk"][:2] = x
+    for k in range(K):
+        pc = dataclasses.replace(ocfg, i_sim=int(iters[k]), epsilon=-1.0)
+        r = cbind.step(x, rho, Uo, pc, gen=None if g0 is None else dataclasses.replace(g0, k0=g0.k0 + k))
+        h["uk"][k] = r["U"][0]
+        h["Uk"][k * N:(k + 1) * N] = r["U"]
+        h["wpred"][k * (N + 1):(k + 1) * (N + 1)] = r["x_pred"][0::2]
+        h["exitflag"][k], h["inner_iters"][k] = r["exitflag"], r["inner_iters"]
+        x, rho, Uo = r["x_next"], r["rho"], r["U_old"]
+        h["xk"][2 * (k + 1):2 * (k + 2)] = x
+    return h
+
+
+def _assert_run_close(out, ref, cfg, k_sim, tol=1e-6, x0=None, ocfg=None, gen=None):
+    """Closed-loop histories of the GPU against the C oracle's.  Mode 3 (rate rows)
+    with ``x0``/``ocfg``: the LPV loop's bitwise stopping rule can fire at another
+    iteration on the two sides, after which the plans part; such a
+    scenario (at most 40% of them) is compared with the oracle replayed along the
+    GPU's iteration counts instead (_replay_along)."""
     N = cfg.N
-    du = np.max(np.abs(H(out["uk"]) - ref["uk"])) / cfg.umax
+    g = {k: H(out[k]) for k in ("uk", "Uk", "xk", "wpred", "exitflag", "inner_iters")}
+    if cfg.mode == 3 and x0 is not None:
+        div = np.where(((g["inner_iters"] != ref["inner_iters"]) | (g["exitflag"] != ref["exitflag"])).any(axis=0))[0]
+        assert len(div) <= 0.4 * x0.shape[1], len(div)
+        ref = {k: np.array(v, copy=True) for k, v in ref.items()}
+        for s in div:
+            rp = _replay_along(x0[:, s], ocfg, g["inner_iters"][:, s], gen, int(s))
+            for k in ref:
+                ref[k][:, s] = rp[k][:, 0]
+    du = np.max(np.abs(g["uk"] - ref["uk"])) / cfg.umax
     assert du <= tol, du
-    dU = np.max(np.abs(H(out["Uk"]) - ref["Uk"])) / cfg.umax
+    dU = np.max(np.abs(g["Uk"] - ref["Uk"])) / cfg.umax
     assert dU <= tol, dU
     xscale = np.tile(np.array([0.15, 2000 * math.pi]), k_sim + 1)[:, None]
-    assert np.max(np.abs(H(out["xk"]) - ref["xk"]) / xscale) <= tol
-    dw = np.max(np.abs(H(out["wpred"]) - ref["wpred"])) / 0.15
+    assert np.max(np.abs(g["xk"] - ref["xk"]) / xscale) <= tol
+    dw = np.max(np.abs(g["wpred"] - ref["wpred"])) / 0.15
     assert dw <= tol, dw
-    assert H(out["wpred"]).shape == ((N + 1) * k_sim, ref["wpred"].shape[1])
-    assert (H(out["exitflag"]) == ref["exitflag"]).mean() > 0.99
+    assert g["wpred"].shape == ((N + 1) * k_sim, ref["wpred"].shape[1])
+    assert (g["exitflag"] == ref["exitflag"]).mean() > 0.99
 
 
 def test_step_matches_run_first_step(ctl):

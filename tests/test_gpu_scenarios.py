@@ -16,7 +16,7 @@ import torch
 from oracle import cbind
 from oracle import ntm_oracle as O
 
-from test_gpu_parity import H, T, _assert_run_close, _teacher_forced, cfgs
+from test_gpu_parity import RUN_TOL, H, T, _assert_run_close, _teacher_forced, cfgs
 
 pytestmark = pytest.mark.gpu
 
@@ -53,7 +53,7 @@ def test_run_with_generator_matches_oracle(ctl, N, mode):
         out = ctl.run(T(x0), k_sim, cfg)
     finally:
         ctl.set_scenarios(None)
-    _assert_run_close(out, ref, cfg, k_sim)
+    _assert_run_close(out, ref, cfg, k_sim, tol=RUN_TOL, x0=x0, ocfg=ocfg, gen=g)
 
 
 def test_initial_state_per_scenario_plasma(ctl):
