@@ -153,7 +153,7 @@ __shared__ int ntm_trace_grp;   // group (of this one-wave block) that owns the 
 // Diagnostic build only (-DNTM_STAMPS): per-phase s_memtime cycle totals,
 // summed over waves into ntm_stamps[] (read with ntm_debug_stamps).  The
 // production library compiles every stamp away.
-#define NTM_NSTAMPS 64
+#define NTM_NSTAMPS 80
 #ifdef NTM_STAMPS
 extern __device__ unsigned long long ntm_stamps[NTM_NSTAMPS];
 __shared__ unsigned long long ntm_lds_stamps[NTM_NSTAMPS];   // per block (= per wave), flushed once
@@ -167,9 +167,9 @@ __shared__ unsigned long long ntm_lds_stamps[NTM_NSTAMPS];   // per block (= per
 #define NTM_CNT(i) \
     do { if ((threadIdx.x & 63) == 0) ntm_lds_stamps[i] += 1ull; } while (0)
 #define NTM_STAMPS_INIT() \
-    do { if (threadIdx.x < NTM_NSTAMPS) ntm_lds_stamps[threadIdx.x] = 0; __syncthreads(); } while (0)
+    do { for (int i_ = threadIdx.x; i_ < NTM_NSTAMPS; i_ += blockDim.x) ntm_lds_stamps[i_] = 0; __syncthreads(); } while (0)
 #define NTM_STAMPS_FLUSH() \
-    do { __syncthreads(); if (threadIdx.x < NTM_NSTAMPS) atomicAdd(&ntm_stamps[threadIdx.x], ntm_lds_stamps[threadIdx.x]); } while (0)
+    do { __syncthreads(); for (int i_ = threadIdx.x; i_ < NTM_NSTAMPS; i_ += blockDim.x) atomicAdd(&ntm_stamps[i_], ntm_lds_stamps[i_]); } while (0)
 #else
 #define NTM_T0(v) (void)0
 #define NTM_ACC(i, v) (void)0
@@ -183,7 +183,8 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        ST_S_E, ST_S_Y, ST_S_K, ST_S_CHOL, ST_S_SOLVE, CN_TRY_EARLY, CN_FAIL_EARLY, CN_FAIL_LATE,
        CN_FAIL_IT1, CN_FAIL_IT2, CN_GI_IT1, CN_GI_IT2, CN_GI_LATE, CN_TRY_IT1, CN_TRY_IT2, CN_WARM_TRY, CN_WARM_OK, CN_WARM_DEP, CN_WARM_NEG, CN_WARM_FULL, CN_ALT_TRY, CN_ALT_HIT,
        ST_K_Y, ST_K_CHK, ST_K_GRAD, ST_K_MU, ST_K_SUB, ST_C_A, ST_C_B, ST_C_Y, ST_C_SQ,
-       ST_SC_COL, ST_SC_ROW, ST_SC_END, ST_L_COEF, ST_L_LOOP, CN_CYC_HIT, CN_CYC_SKIP };
+       ST_SC_COL, ST_SC_ROW, ST_SC_END, ST_L_COEF, ST_L_LOOP, CN_CYC_HIT, CN_CYC_SKIP,
+       CN_FK_DUAL, CN_FK_PRIMAL, CN_FK_SING, CN_FK_BOTH };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 #ifndef NTM_MAX_NT
 #define NTM_MAX_NT 32
@@ -2441,6 +2442,53 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             return c;
         };
         double* const Ep = w.Ep();
+        // long horizons: lane t builds sorted row t (n <= N <= 64 rows).  The row's
+        // constants (its general row, sign, norm) are loaded once, and each batch of
+        // CH columns costs one LDS round trip: the column index and D_j are the same
+        // address on every lane (broadcast reads), only Gamma_rj differs.  The entry-
+        // per-lane loop below issues ~5 dependent loads per entry, n^2 / 64 times per
+        // lane (n ~ 43 at N = 50).  Entries as gen_n computes them, bit for bit.
+        constexpr bool kRowE = W::kNN > 32 || W::kNN == 0;
+        if constexpr (kRowE) {
+            if (l < n) {
+                const int s2 = perm[l];
+                const int r = w.srw()[s2];
+                const double sg = w.ssg()[s2];
+                double* const erow = Ep + w.eidx(l, 0);
+                constexpr int CH = NTM_CH;
+                if (r >= 2 * N) {                                  // rate row of input i
+                    const int i = r - 2 * N;
+                    const double ir = w.idun()[i];
+                    for (int u = 0; u <= l; ++u) {
+                        const int j = w.fidx()[pc(u)];
+                        const double lv = (j == i) ? sg : (j == i - 1 ? -sg : 0.0);
+                        erow[u] = -((lv * w.D()[j]) * ir);
+                    }
+                } else {
+                    const double ir = w.irn()[r];
+                    const int jm = r >> 1;
+                    const double* gr = w.Gt() + r;                 // gt(r, j) = gr[gidx(0, j)]
+                    for (int u0 = 0; u0 <= l; u0 += CH) {
+                        int jj[CH];
+                        double g[CH], d[CH];
+#pragma unroll
+                        for (int c = 0; c < CH; ++c) jj[c] = (u0 + c <= l) ? w.fidx()[pc(u0 + c)] : 0;
+#pragma unroll
+                        for (int c = 0; c < CH; ++c) {
+                            const bool in = u0 + c <= l && jj[c] <= jm;
+                            g[c] = in ? gr[w.gidx(0, jj[c])] : 0.0;
+                            d[c] = (u0 + c <= l) ? w.D()[jj[c]] : 0.0;
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int c = 0; c < CH; ++c)
+                            if (u0 + c <= l) erow[u0 + c] = (jj[c] <= jm) ? -(((sg * g[c]) * d[c]) * ir) : 0.0;
+                    }
+                }
+                if constexpr (!W::kFar)
+                    for (int u = l + 1; u < n; ++u) erow[u] = 0.0;
+            }
+        } else {
         for (int idx = l; idx < n * n; idx += P) {
             const int t = idx / n, u = idx - t * n;
             if constexpr (W::kFar) {                               // packed: the lower triangle only
@@ -2448,6 +2496,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             } else {
                 Ep[w.eidx(t, u)] = (u <= t) ? gen_n(perm[t], w.fidx()[pc(u)]) : 0.0;
             }
+        }
         }
         double acc = 0.0, acz = 0.0, acz2 = 0.0;
         if (l < n) {
@@ -3281,6 +3330,12 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                     if (rep == 0) {
                         if (it <= 2) NTM_CNT(CN_TRY_EARLY);
                         if (!okc) { if (it <= 2) NTM_CNT(CN_FAIL_EARLY); else NTM_CNT(CN_FAIL_LATE); }
+                        if (it <= 2 && !okc) {
+                            if (fk == 1) NTM_CNT(CN_FK_DUAL);
+                            else if (fk == 2) NTM_CNT(CN_FK_PRIMAL);
+                            else if (fk == 3) NTM_CNT(CN_FK_SING);
+                            else NTM_CNT(CN_FK_BOTH);
+                        }
                         if (it == 1) { NTM_CNT(CN_TRY_IT1); if (!okc) NTM_CNT(CN_FAIL_IT1); }
                         if (it == 2) { NTM_CNT(CN_TRY_IT2); if (!okc) NTM_CNT(CN_FAIL_IT2); }
                     }

@@ -10,7 +10,7 @@ N = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 cfg = Config(N=N, mode=int(sys.argv[3]) if len(sys.argv) > 3 else 2)
 ctl = NtmMpc(config=cfg)
 lib = ntm_mpc.load()
-buf = (C.c_ulonglong * 64)()
+buf = (C.c_ulonglong * 80)()
 x = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(0, B))
 rho, uo = ctl.initial_state(x, cfg)
 ws = ctl.new_active_ws(B, cfg)
@@ -42,10 +42,12 @@ print(f"per wave-step: tries it=1 {buf[37]/B:.2f} failed {buf[32]/B:.2f}; tries 
       f"GI solves at it=1 {buf[34]/B:.2f}, it=2 {buf[35]/B:.2f}, later {buf[36]/B:.2f}")
 print(f"per wave-step: GI warm starts tried {buf[39]/B:.2f}, accepted {buf[40]/B:.2f}")
 print(f"  dependent rows skipped {buf[41]/B:.3f}; rejected: negative multiplier {buf[42]/B:.3f}; stopped at N rows {buf[43]/B:.3f}")
-print(f"per wave-step: shifted second candidate at it=2 tried {buf[44]/B:.2f}, hits {buf[45]/B:.2f}")
+print(f"per wave-step: the other form (shifted or unshifted) of the carried set at it=2 tried {buf[44]/B:.2f}, hits {buf[45]/B:.2f}")
 fine = "k_y k_chk k_grad k_mu k_sub c_a c_b c_y c_sq sc_col sc_row sc_end l_coef l_loop".split()
 print("certificate / classification detail, cycles per wave-step:")
 for i, n in enumerate(fine):
     print(f"  {n:9s} {buf[46 + i]/B:12.0f}")
 print(f"exact 2-cycle study: steps whose rho and U after iteration it equal those after it-2 (it >= 3): "
       f"{buf[60]/B:.4f} per wave-step; iterations a shortcut could skip {buf[61]/B:.4f} per wave-step")
+print(f"first tries at it<=2 that failed, by kind, per wave-step: dual {buf[62]/B:.3f}, primal {buf[63]/B:.3f}, "
+      f"singular/colliding {buf[64]/B:.3f}, primal and dual {buf[65]/B:.3f}")
