@@ -3311,6 +3311,11 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                     if (l < cq) w.act()[l] = cand[l];
                     NTM_WSYNC();
                 }
+#ifdef NTM_DEBUG_SCEN
+                NTM_TRACE("SET it %d cand %d:", it, cq);
+                for (int i = 0; i < cq; ++i) NTM_TRACE(" %d", w.act()[i]);
+                NTM_TRACE("\n");
+#endif
                 // iteration 2: the carried set is the previous step's (slot 1 is only
                 // written at even iterations); when its repairs fail, its
                 // receding-horizon shift is tried before GI (it hits in the
@@ -3470,6 +3475,11 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
         if (l == 0) cand[N] = q;
     }
     NTM_WSYNC();
+#ifdef NTM_DEBUG_SCEN
+    NTM_TRACE("SET it %d final %d flag %d:", it, flag == NTM_EXIT_OPTIMAL ? q : -1, flag);
+    for (int i = 0; flag == NTM_EXIT_OPTIMAL && i < q; ++i) NTM_TRACE(" %d", cand[i]);
+    NTM_TRACE("\n");
+#endif
     if (q_out) *q_out = q;
     if (ns_out) *ns_out = ns;
     return flag;
