@@ -247,6 +247,10 @@ def test_step_layout_by_batch(ctl):
     lit = Config(N=20, mode=2, flags=1)
     assert ctl.step_layout(100_000, lit) == "lds" and ctl.step_kernel_name(100_000, lit) == "k_mpc_step<P=64,NN=0,lds>"
     assert ctl.step_kernel_name(100_000, c20) == "k_mpc_step<P=64,NN=20,far>"
+    # N = 20 with input-rate rows runs on the generic kernel too (its collision paths
+    # and refined bordered re-solve keep mode 3 within 1e-10)
+    assert ctl.step_kernel_name(100_000, Config(N=20, mode=3)) == "k_mpc_step<P=64,NN=0,lds>"
+    assert ctl.step_kernel_name(100_000, Config(N=50, mode=3)) == "k_mpc_step<P=64,NN=50,far>"
     ctl.set_small_batch(0)
     try:
         assert ctl.step_layout(1, c20) == "far"
