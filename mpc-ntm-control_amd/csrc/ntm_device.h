@@ -3375,23 +3375,35 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                             if ((kind == 2 || kind == 3) && jr >= 0) jl = (w.rinfo()[jr] & (kRowMulti - 1)) - 1;
                             else if (kind >= 4) jl = jr;
                             int my = -1;
-                            bool drop_me = false;
+                            bool drop_me = false, rate_hold = false;
+                            // rate rows (long horizons and the generic kernels): a u bound on
+                            // input jb entering a full set replaces the one active rate row that
+                            // holds jb (U_i - U_{i-1} with i or i-1 = jb).  With rate rows the
+                            // odd LPV iterations can alternate between two sets that differ in
+                            // exactly that pair (a period-4 cycle), and the
+                            // smallest-multiplier swap below would pick another row
+                            constexpr bool kRateSwap = W::kNN > 32 || W::kNN == 0;
+                            const int jb = (kRateSwap && kind < 2) ? jr : -1;
                             if (l < cq) {
                                 my = w.act()[l];
                                 int k2, j2;
                                 rows.decode(my, N, k2, j2);
                                 drop_me = (jl >= 0 && k2 < 2 && j2 == jl) || (fk == 4 && l == fp);
+                                rate_hold = jb >= 0 && k2 >= 4 && (j2 == jb || j2 - 1 == jb);
                             }
                             const int lane = threadIdx.x & 63;
                             const unsigned long long gm =
                                 (P == 64) ? ~0ull : (((1ull << P) - 1ull) << (lane & ~(P - 1)));
                             const unsigned long long keepm = __ballot(l < cq && !drop_me) & gm;
                             const int nkeep = uni<P>((int)__popcll(keepm));
+                            const unsigned long long rhm = kRateSwap ? (__ballot(rate_hold) & gm) : 0ull;
                             NTM_WSYNC();
                             if (nkeep < N) {
                                 if (l < cq && !drop_me) w.act()[__popcll(keepm & ((1ull << lane) - 1ull))] = my;
                                 if (l == 0) w.act()[nkeep] = pk.p;
                                 cq = nkeep + 1;
+                            } else if (kRateSwap && __popcll(rhm) == 1) {   // a full set: the rate row holding jb
+                                if (rate_hold) w.act()[l] = pk.p;
                             } else if (l == 0) {           // a full set: swap out the smallest multiplier
                                 w.act()[fp] = pk.p;
                             }
