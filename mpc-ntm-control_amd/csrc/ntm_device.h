@@ -3378,7 +3378,8 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                             bool drop_me = false, rate_hold = false;
                             // rate rows (long horizons and the generic kernels): a u bound on
                             // input jb entering a full set replaces the one active rate row that
-                            // holds jb (U_i - U_{i-1} with i or i-1 = jb).  With rate rows the
+                            // holds jb (U_i - U_{i-1} with i or i-1 = jb), and a rate row entering
+                            // one replaces the bound on its earlier input.  With rate rows the
                             // odd LPV iterations can alternate between two sets that differ in
                             // exactly that pair (a period-4 cycle), and the
                             // smallest-multiplier swap below would pick another row
@@ -3390,6 +3391,9 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                                 rows.decode(my, N, k2, j2);
                                 drop_me = (jl >= 0 && k2 < 2 && j2 == jl) || (fk == 4 && l == fp);
                                 rate_hold = jb >= 0 && k2 >= 4 && (j2 == jb || j2 - 1 == jb);
+                                // and a rate row of input jr entering a full set replaces the
+                                // u bound on input jr - 1 (the one on jr is dropped above)
+                                if (kRateSwap && kind >= 4 && k2 < 2 && j2 == jr - 1) rate_hold = true;
                             }
                             const int lane = threadIdx.x & 63;
                             const unsigned long long gm =
