@@ -9,7 +9,7 @@ import os
 import sys
 
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
-os.environ["NTM_MPC_LIB"] = os.path.join(ROOT, "mpc-ntm-control_amd", "lib", "libntm_mpc_trace.so")
+os.environ.setdefault("NTM_MPC_LIB", os.path.join(ROOT, "mpc-ntm-control_amd", "lib", "libntm_mpc_trace.so"))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "mpc-ntm-control_amd")]
 import torch  # noqa: E402
 
