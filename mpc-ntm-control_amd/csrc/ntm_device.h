@@ -184,7 +184,7 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        CN_FAIL_IT1, CN_FAIL_IT2, CN_GI_IT1, CN_GI_IT2, CN_GI_LATE, CN_TRY_IT1, CN_TRY_IT2, CN_WARM_TRY, CN_WARM_OK, CN_WARM_DEP, CN_WARM_NEG, CN_WARM_FULL, CN_ALT_TRY, CN_ALT_HIT,
        ST_K_Y, ST_K_CHK, ST_K_GRAD, ST_K_MU, ST_K_SUB, ST_C_A, ST_C_B, ST_C_Y, ST_C_SQ,
        ST_SC_COL, ST_SC_ROW, ST_SC_END, ST_L_COEF, ST_L_LOOP, CN_CYC_HIT, CN_CYC_SKIP,
-       CN_FK_DUAL, CN_FK_PRIMAL, CN_FK_SING, CN_FK_BOTH };
+       CN_FK_DUAL, CN_FK_PRIMAL, CN_FK_SING, CN_FK_BOTH, ST_GI_WARM };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 #ifndef NTM_MAX_NT
 #define NTM_MAX_NT 32
@@ -1747,6 +1747,7 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
             return kGiWarmRejected;                        // *q_out: rows kept in w.sidx() (0: none)
         }
     }
+    NTM_ACC(ST_GI_WARM, tg);                               // the warm start's adds (not the first check)
     for (;;) {
         const double vmax = gmax<P>(l < N ? fabs(Vl) : 0.0);
         Pick pk = rows.template check<P>(w, Vl, l, false, fmax(1.0, vmax));

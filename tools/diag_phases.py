@@ -40,7 +40,8 @@ for i, n in enumerate(sch):
     print(f"    {n:9s} {buf[24 + i]/B:12.0f}")
 print(f"per wave-step: tries it=1 {buf[37]/B:.2f} failed {buf[32]/B:.2f}; tries it=2 {buf[38]/B:.2f} failed {buf[33]/B:.2f}; "
       f"GI solves at it=1 {buf[34]/B:.2f}, it=2 {buf[35]/B:.2f}, later {buf[36]/B:.2f}")
-print(f"per wave-step: GI warm starts tried {buf[39]/B:.2f}, accepted {buf[40]/B:.2f}")
+print(f"per wave-step: GI warm starts tried {buf[39]/B:.2f}, accepted {buf[40]/B:.2f}; "
+      f"warm-start adds {buf[66]/B:.0f} cycles (inside gi, apart from gi_check)")
 print(f"  dependent rows skipped {buf[41]/B:.3f}; rejected: negative multiplier {buf[42]/B:.3f}; stopped at N rows {buf[43]/B:.3f}")
 print(f"per wave-step: the other form (shifted or unshifted) of the carried set at it=2 tried {buf[44]/B:.2f}, hits {buf[45]/B:.2f}")
 fine = "k_y k_chk k_grad k_mu k_sub c_a c_b c_y c_sq sc_col sc_row sc_end l_coef l_loop".split()
