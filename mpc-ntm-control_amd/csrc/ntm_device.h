@@ -190,7 +190,10 @@ constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_
 #define NTM_MAX_NT 32
 #endif
 constexpr int kMaxNT = NTM_MAX_NT; // explicit R^{-1} in GI up to this horizon (WS::useT)
-constexpr int kRepairs = 8;   // also at N = 50: 16 / 32 were no faster in mode 2, 6% / 10% slower in mode 3
+#ifndef NTM_REPAIRS
+#define NTM_REPAIRS 8
+#endif
+constexpr int kRepairs = NTM_REPAIRS;   // also at N = 50: 16 / 32 were no faster in mode 2, 6% / 10% slower in mode 3
 // A constant row (Lin_i = 0: the x_0 rows of getWLc, state rows Gamma doesn't
 // reach) is violated when b_i < -kConstTol (D22, oracle CONST_ROW_TOL): the same
 // absolute 1e-9 the KKT certificate allows on a unit-scale row.  An exact test
