@@ -293,11 +293,18 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - leg["t0"]
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearsal else f"cuda:{local}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
     r = _finish_leg(ctl, leg, K)
+    # per-rank timings: each rank's own wall time of the K steps and
+    # its HIP-event kernel average, so a scaling run shows which rank set the max
+    per_rank = {"elapsed_s": [elapsed], "kernel_avg_ms": [r["kern_ms"]]}
+    if world > 1:
+        tdev = "cpu" if rehearsal else f"cuda:{local}"
+        mine = torch.tensor([elapsed, r["kern_ms"]], dtype=torch.float64, device=tdev)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = {"elapsed_s": [float(t[0].item()) for t in allr],
+                    "kernel_avg_ms": [float(t[1].item()) for t in allr]}
+        elapsed = max(per_rank["elapsed_s"])                  # the max over ranks
     if world == 1:
         g = leg["hist"]
     verify = None
@@ -362,6 +369,9 @@ def main():
                    "gi_iters_per_step": r["Kgi"], "active_rows_per_qp": r["qact"], "state_rows_per_qp": r["sgen"],
                    "warm_hit_rate": 1.0 - r["giruns"] / r["qps"], "optimal_frac": r["optimal_frac"]},
         "gather_verify": verify,
+        "per_rank": {**per_rank, "kernel_avg_ms_max": max(per_rank["kernel_avg_ms"]),
+                     "note": "elapsed_s: each rank's wall time of the K timed steps (barrier + synchronize "
+                             "bracketed, gather included); value uses their max"},
     }
     if not args.no_disturbed:
         gen = ScenarioGen(seed=20241220, first_id=rank * B, k0=0, sigma_w=args.sigma_w, sigma_omega=0.0,

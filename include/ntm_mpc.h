@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define NTM_MPC_ABI_VERSION 4   /* v4: ntm_scenario_gen (ABI v3 arrays unchanged) */
+#define NTM_MPC_ABI_VERSION 5   /* v5: ntm_config.Ru (input weight); v4: ntm_scenario_gen */
 #define NTM_MAX_N 64
 
 /* Physics constants, NTM_MPC_Sim.m:5-22 (same names and units). */
@@ -76,6 +76,11 @@ typedef struct {
     double r[2];        /* :60 reference state                             */
     double epsilon;     /* :87 convergence threshold on sum|U - Uold|      */
     double du_max;      /* NTM_MODE_FULL_DU only: input-rate bound (W/step) */
+    double Ru;          /* input weight R_u >= 0: the cost of
+                         * NTM_MPC_Sim.m:71-73,120 becomes G = 2 Gamma' Om Gamma
+                         * + 2 Ru I (F unchanged).  The reference has none: 0,
+                         * its default, is the reference's cost (ABI v5).  A
+                         * non-zero Ru runs on the generic (runtime-N) kernels. */
 } ntm_config;
 
 /* Return codes. */

@@ -33,7 +33,8 @@
  *   ntm_mpc_mex('close')
  *
  * cfg is an optional struct with any of the fields N, i_sim, mode, flags, Ts,
- * xmin, xmax, umin, umax, Q (2x2), r, epsilon, du_max; missing fields take the
+ * xmin, xmax, umin, umax, Q (2x2), r, epsilon, du_max, Ru (input weight, ABI v5);
+ * missing fields take the
  * reference literals (ntm_config_default).  Library errors become MATLAB
  * errors (ntm:...); solver outcomes are returned in exitflag (quadprog codes,
  * NTM_MPC_Sim.m:98-103), never raised.
@@ -90,6 +91,7 @@ static ntm_config read_cfg(const mxArray* s) {
     c.umax = scalar_field(s, "umax", c.umax);
     c.epsilon = scalar_field(s, "epsilon", c.epsilon);
     c.du_max = scalar_field(s, "du_max", c.du_max);
+    c.Ru = scalar_field(s, "Ru", c.Ru);
     vec_field(s, "xmin", c.xmin, 2);
     vec_field(s, "xmax", c.xmax, 2);
     vec_field(s, "r", c.r, 2);

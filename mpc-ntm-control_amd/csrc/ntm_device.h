@@ -65,11 +65,14 @@ struct Prob {
     int N, i_sim, mode, flags;
     double xmin[2], xmax[2], umin, umax, Q[4], r[2], eps;
     double du;        // input-rate bound (NTM_MODE_FULL_DU)
-    int32_t* stats;   // optional per-scenario counters (4 x B, SoA): QP solves,
+    int32_t* stats;  // optional per-scenario counters (4 x B, SoA): QP solves,
                       // GI iterations, final active rows, general (state) active rows
     Gen g;
     double* far;      // far workspace (HBM, far_doubles(N) per scenario) of the kernels
                       // whose WS keeps J/R out of LDS (ws_far); null otherwise
+    double Ru;        // input weight (ABI v5): G = 2 Gamma' Om Gamma + 2 Ru I; read by the
+                      // generic (NN = 0) kernels only, the host sends Ru != 0 there (ru_on);
+                      // last, so the specialised kernels' argument layout is unchanged
 };
 
 constexpr double kInf = __builtin_huge_val();
@@ -577,6 +580,18 @@ __device__ inline WS<NN, GEN, FAR> ws_carve(char* base, int N, const Prob* pb = 
 // (written once per launch by scn_store).  Keeping the launch constants in the
 // kernel arguments matters: a copy of the whole Prob per scenario cost the N=20
 // step kernel 100 B of scratch per lane and 20 more spilled SGPRs.
+// The input weight R_u: its term 2 Ru I of the Hessian enters the
+// Gram diagonal (scaling, GI's full G~, the re-solve's G~_FF), the echelon k = 1 line
+// search and the certificate's gradient.  Compiled into the generic kernels only
+// (ru_on): the specialised N = 10 / 20 / 50 kernels keep their register allocation,
+// and the host dispatches a launch with Ru != 0 to the generic ones (as D4 / D6)
+template <class W>
+__device__ __forceinline__ constexpr bool ru_on() { return W::kNN == 0; }
+template <class W>
+__device__ __forceinline__ double ru_of(const Prob& pb) {
+    if constexpr (ru_on<W>()) return pb.Ru;
+    else return 0.0;
+}
 __device__ __forceinline__ bool gen_phys(const Prob& pb) { return pb.g.phys_on != 0; }
 __device__ __forceinline__ bool gen_dist(const Prob& pb) { return pb.g.dist_on != 0; }
 template <class W>
@@ -1074,7 +1089,9 @@ __device__ __forceinline__ void gram_rows(const Prob& pb, const W& w, double* ds
             const double t = cj[2 * i] * o0 + cj[2 * i + 1] * o1;
             s += (i >= j) ? t : 0.0;
         }
-        dst[j + kk * LD] = 2 * s;   // G(j, kk), j >= kk
+        double gv = 2 * s;
+        if constexpr (ru_on<W>()) gv = (j == kk) ? gv + 2 * pb.Ru : gv;   // + 2 Ru I (ABI v5)
+        dst[j + kk * LD] = gv;      // G(j, kk), j >= kk
     }
 }
 
@@ -1161,6 +1178,7 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
             }
         }
         double g = 2 * s;
+        if constexpr (ru_on<W>()) g = g + 2 * pb.Ru;   // G_ll + 2 Ru (ABI v5)
         double Dl = (g > 0.0 && g < kInf) ? rsqrt_nr(g) : 1.0;
         w.D()[l] = Dl;
         double f = (2 * fs) * Dl;
@@ -2391,7 +2409,9 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             const double* ca = w.Gt() + w.gidx(2 * ja, ja) - 2 * ja;
             const double* cc = w.Gt() + w.gidx(2 * jc, jc) - 2 * jc;
             const double sg = qdot_rows<NTM_CH>(ca, cc, N, ja, q00, q01, q10, q11);   // terms i < ja masked
-            const double gv = (2 * sg) * w.D()[ja] * w.D()[jc];
+            double g2v = 2 * sg;
+            if constexpr (ru_on<W>()) g2v = (a == c) ? g2v + 2 * pb.Ru : g2v;      // + 2 Ru I
+            const double gv = g2v * w.D()[ja] * w.D()[jc];
             if (fused) Lp[w.brow(a) + w.bcol(c, nt)] = gv;            // row-major: idx == a(a+1)/2 + c
             else w.R()[a + c * LD] = gv;
         }
@@ -2596,6 +2616,11 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 const double oa = q00 * za + q01 * zb, ob = q10 * za + q11 * zb;
                 num = oa * y0a + ob * y0b;
                 den = oa * za + ob * zb;
+                if constexpr (ru_on<W>()) {               // Ru (dU' U_0, dU' dU): w.U() = D V_0, w.d() = D Z
+                    const double ua = w.U()[l], da = w.d()[l];
+                    num += pb.Ru * (da * ua);
+                    den += pb.Ru * (da * da);
+                }
             }
             num = gsum<P>(num);
             den = gsum<P>(den);
@@ -2944,7 +2969,9 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         if (l < N) {
             const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;
             const double g2 = dot_rows2<NTM_CH>(cl, w.xp(), N, l);   // terms i < l masked
-            res = w.D()[l] * (2 * g2) + w.F()[l];
+            double gu = 2 * g2;
+            if constexpr (ru_on<W>()) gu = gu + 2 * pb.Ru * w.U()[l];  // + 2 Ru U_l
+            res = w.D()[l] * gu + w.F()[l];
         }
         NTM_ACC(ST_K_GRAD, tp);
         if (sq) {

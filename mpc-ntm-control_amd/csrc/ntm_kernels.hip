@@ -336,6 +336,7 @@ Prob make_prob(const ntm_physics* p, const ntm_config* c) {
     pb.mode = c->mode;
     pb.flags = c->flags;
     pb.du = c->du_max;
+    pb.Ru = c->Ru;
     for (int i = 0; i < 2; ++i) {
         pb.xmin[i] = c->xmin[i];
         pb.xmax[i] = c->xmax[i];
@@ -446,6 +447,7 @@ int validate(ntm_ctx* ctx, const ntm_physics* p, const ntm_config* c, int64_t B)
     if (c->mode < NTM_MODE_NONE || c->mode > NTM_MODE_FULL_DU) return fail(ctx, NTM_E_INVALID, "bad mode");
     if (c->mode == NTM_MODE_FULL_DU && !(std::isfinite(c->du_max)))
         return fail(ctx, NTM_E_INVALID, "du_max must be finite");
+    if (!(std::isfinite(c->Ru) && c->Ru >= 0.0)) return fail(ctx, NTM_E_INVALID, "Ru must be finite and >= 0");
     if (B < 0) return fail(ctx, NTM_E_INVALID, "negative batch");
     return NTM_OK;
 }
@@ -608,8 +610,11 @@ bool force_generic() {
 // N = 20 kernel would take there factors a nearly singular G~_FF (the last inputs
 // act almost alike) and sat up to ~1e-8 umax off the exact optimum; compiled into
 // the N = 20 kernel the paths cost mode 2 ~1% through register allocation.
+// The input weight Ru (ABI v5) is compiled into the generic kernels only (ru_on in
+// ntm_device.h), like D4 / D6: the reference's cost has none (Ru = 0).
 bool use_generic(const ntm_config* c) {
-    return force_generic() || (c->flags & kGenericOnlyFlags) != 0 || (c->N == 20 && c->mode == NTM_MODE_FULL_DU);
+    return force_generic() || (c->flags & kGenericOnlyFlags) != 0 || (c->N == 20 && c->mode == NTM_MODE_FULL_DU) ||
+           c->Ru != 0.0;
 }
 #ifdef NTM_RU_ONLY20
 // resource-usage check of the N=20 hot kernel alone (make ru20): every horizon

@@ -14,7 +14,7 @@ LIB_PATH = Path(os.environ.get("NTM_MPC_LIB", PKG_ROOT / "lib" / "libntm_mpc.so"
 
 MAX_N = 64
 MODE_NONE, MODE_BOX, MODE_FULL, MODE_FULL_DU = 0, 1, 2, 3
-ABI_VERSION = 4          # include/ntm_mpc.h NTM_MPC_ABI_VERSION
+ABI_VERSION = 5          # include/ntm_mpc.h NTM_MPC_ABI_VERSION
 LITERAL_PHI_RIGHTMUL, LITERAL_GAMMA_INDEX, LITERAL_PLANT_NO_C, RHO1_SQUARED = 1, 2, 4, 8
 EXIT_OPTIMAL, EXIT_MAXITER, EXIT_INFEASIBLE, EXIT_NONFINITE = 1, 0, -2, -7
 NTM_OK = 0
@@ -37,7 +37,8 @@ class NtmConfig(C.Structure):
     _fields_ = [("N", C.c_int32), ("i_sim", C.c_int32), ("mode", C.c_int32), ("flags", C.c_int32),
                 ("Ts", C.c_double), ("xmin", C.c_double * 2), ("xmax", C.c_double * 2),
                 ("umin", C.c_double), ("umax", C.c_double), ("Q", C.c_double * 4),
-                ("r", C.c_double * 2), ("epsilon", C.c_double), ("du_max", C.c_double)]
+                ("r", C.c_double * 2), ("epsilon", C.c_double), ("du_max", C.c_double),
+                ("Ru", C.c_double)]
 
 
 class NtmScenarioGen(C.Structure):

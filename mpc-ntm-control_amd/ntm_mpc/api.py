@@ -84,12 +84,13 @@ class Config:
     mode: int = L.MODE_FULL
     flags: int = 0
     du_max: float = 5e5      # NTM_MODE_FULL_DU (config 5, extension): |U_i - U_{i-1}| <= du_max
+    Ru: float = 0.0          # input weight (ABI v5): G = 2 Gamma' Om Gamma + 2 Ru I; the reference: 0
 
     def to_c(self) -> NtmConfig:
         return NtmConfig(int(self.N), int(self.i_sim), int(self.mode), int(self.flags), float(self.Ts),
                          (C.c_double * 2)(*self.xmin), (C.c_double * 2)(*self.xmax), float(self.umin),
                          float(self.umax), (C.c_double * 4)(*self.Q), (C.c_double * 2)(*self.r),
-                         float(self.epsilon), float(self.du_max))
+                         float(self.epsilon), float(self.du_max), float(self.Ru))
 
     @property
     def m(self) -> int:

@@ -29,7 +29,8 @@ class CCfg(C.Structure):
     _fields_ = [("N", C.c_int32), ("i_sim", C.c_int32), ("mode", C.c_int32), ("flags", C.c_int32),
                 ("Ts", C.c_double), ("xmin", C.c_double * 2), ("xmax", C.c_double * 2),
                 ("umin", C.c_double), ("umax", C.c_double), ("Q", C.c_double * 4),
-                ("r", C.c_double * 2), ("epsilon", C.c_double), ("du_max", C.c_double)]
+                ("r", C.c_double * 2), ("epsilon", C.c_double), ("du_max", C.c_double),
+                ("Ru", C.c_double)]
 
 
 class CGen(C.Structure):
@@ -68,7 +69,7 @@ def phys_c(ph: O.Physics | None = None) -> CPhys:
 def cfg_c(cfg: O.Config) -> CCfg:
     return CCfg(cfg.N, cfg.i_sim, cfg.mode, cfg.flags, cfg.Ts, (C.c_double * 2)(*cfg.xmin),
                 (C.c_double * 2)(*cfg.xmax), cfg.umin, cfg.umax, (C.c_double * 4)(*cfg.Q),
-                (C.c_double * 2)(*cfg.r), cfg.epsilon, cfg.du_max)
+                (C.c_double * 2)(*cfg.r), cfg.epsilon, cfg.du_max, cfg.Ru)
 
 
 def _dp(a):

@@ -162,7 +162,7 @@ static void orc_lift(const orc_coef* k, const ntm_config* c, const double* rho,
     }
 }
 
-/* NTM_MPC_Sim.m:71-73,120-121: G = 2 Gam' Om Gam, F = 2 Gam' Om (Phi x + Lam - R). */
+/* NTM_MPC_Sim.m:71-73,120-121: G = 2 Gam' Om Gam (+ 2 Ru I), F = 2 Gam' Om (Phi x + Lam - R). */
 static void orc_cost(const ntm_config* c, const double* Phi, const double* Gam,
                      const double* Lam, const double* x, double* G, double* F) {
     int N = c->N, R = 2 * N;
@@ -180,6 +180,9 @@ static void orc_cost(const ntm_config* c, const double* Phi, const double* Gam,
             for (int r = 0; r < R; ++r) s += Gam[(size_t)a * R + r] * OG[(size_t)b * R + r];
             G[(size_t)b * N + a] = 2 * s;
         }
+    /* input weight (ABI v5): G += 2 Ru I; the reference has Ru = 0 */
+    if (c->Ru != 0.0)
+        for (int a = 0; a < N; ++a) G[(size_t)a * N + a] = G[(size_t)a * N + a] + 2 * c->Ru;
     double e[2 * NMAX];
     for (int i = 0; i < N; ++i) {
         e[2 * i] = (Phi[2 * i] * x[0] + Phi[R + 2 * i] * x[1]) + Lam[2 * i] - c->r[0];

@@ -103,6 +103,7 @@ class Config:
     mode: int = MODE_FULL
     flags: int = 0
     du_max: float = 5e5                          # MODE_FULL_DU only (W per step)
+    Ru: float = 0.0                              # input weight (ABI v5); the reference: 0
 
     @property
     def m_rows(self) -> int:
@@ -226,10 +227,14 @@ def omega_blk(cfg: Config):
 
 def cost(Phi, Gamma, Lam, xk, cfg: Config):
     """NTM_MPC_Sim.m:71-73 / :120-121:  G = 2 Gamma' Omega Gamma,
-    F = 2 Gamma' Omega (Phi x_k + Lambda - R), R = [r; ...; r] (D8), x_k not x0 (D12)."""
+    F = 2 Gamma' Omega (Phi x_k + Lambda - R), R = [r; ...; r] (D8), x_k not x0 (D12).
+    With an input weight R_u (D17, "Q, R_u exposed in config"; the reference has none,
+    NTM_MPC_Sim.m:59,72) the cost sum x'Qx + R_u u^2 adds 2 R_u I to G; F is unchanged."""
     Om = omega_blk(cfg)
     R = np.tile(np.array(cfg.r, dtype=float), cfg.N)
     G = 2 * Gamma.T @ Om @ Gamma
+    if cfg.Ru != 0.0:
+        G = G + 2 * cfg.Ru * np.eye(cfg.N)
     F = 2 * Gamma.T @ Om @ (Phi @ xk + Lam - R)
     return G, F
 

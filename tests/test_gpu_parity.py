@@ -111,10 +111,11 @@ def test_lift_matches_oracle(ctl, N):
 
 
 # ---------------------------------------------------------------- a9
-@pytest.mark.parametrize("N", [3, 20, 50])
-def test_cost_matches_oracle(ctl, N):
+@pytest.mark.parametrize("N,Ru", [(3, 0.0), (20, 0.0), (50, 0.0), (20, 1e-10), (3, 1e-9)])
+def test_cost_matches_oracle(ctl, N, Ru):
+    """G and F of NTM_MPC_Sim.m:120-121 (+ 2 Ru I with an input weight, ABI v5)."""
     B = 17
-    cfg, ocfg = cfgs(N, 2)
+    cfg, ocfg = cfgs(N, 2, Ru=Ru)
     rho = random_rho(N, B, 5)
     x = random_states(B, 6)
     G, F = (H(t) for t in ctl.cost(T(rho), T(x), cfg))
@@ -206,6 +207,46 @@ def test_step_teacher_forced(ctl, N, mode, warm):
 @pytest.mark.parametrize("N,mode,warm", [(20, 2, True), (20, 1, False), (50, 2, False), (3, 2, False)])
 def test_step_teacher_forced_weighted(ctl, N, mode, warm):
     _teacher_forced(ctl, N, mode, warm, k_sim=6, Q=(2.0e4, 3.0, 3.0, 2.0e-2), r=(0.09, 900 * 2 * math.pi))
+
+
+# Input weight R_u (ABI v5; SURVEY §2.1 D17 "Q, R_u exposed in config"; the reference's
+# cost has none, NTM_MPC_Sim.m:59,72-73): G = 2 Gamma' Om Gamma + 2 Ru I on both sides
+# (oracle cost / orc_cost).  The weights span the range where the plan moves (oracle,
+# first step, 32 scenarios at N = 20 mode 2: Ru = 1e-11 moves U by 2e-4 umax, 1e-10 by
+# 2e-3, 1e-9 by 0.70, i.e. the input cost takes over from the bang-bang plan); the
+# smallest eigenvalue of the Ru = 0 Hessian is 3.9e-17.  The launches
+# run on the generic kernels (the host dispatch), in every mode.
+@pytest.mark.parametrize("N,mode,warm,Ru", [(20, 2, True, 1e-10), (20, 2, False, 1e-9), (20, 1, False, 1e-9),
+                                            (50, 3, True, 1e-10), (3, 2, False, 1e-9), (10, 2, False, 1e-11),
+                                            (20, 3, True, 1e-9)])
+def test_step_teacher_forced_input_weight(ctl, N, mode, warm, Ru):
+    _teacher_forced(ctl, N, mode, warm, Ru=Ru)
+
+
+def test_input_weight_changes_the_plan_and_dispatch(ctl):
+    """Ru != 0 is not a no-op (the plans move by far more than the parity tolerance),
+    runs on the generic kernel, and Ru = 0 stays on the specialised one."""
+    from ntm_mpc import Config
+    assert ctl.step_kernel_name(100_000, Config(N=20, mode=2, Ru=1e-10)) == "k_mpc_step<P=64,NN=0,lds>"
+    assert ctl.step_kernel_name(100_000, Config(N=20, mode=2, Ru=0.0)) == "k_mpc_step<P=64,NN=20,far>"
+    B = 32
+    x = O.scenario_x0(np.arange(B)).T
+    outs = []
+    for Ru in (0.0, 1e-10):
+        cfg, ocfg = cfgs(20, 2, Ru=Ru)
+        rho, Uo = cbind.initial_state(x, ocfg)
+        outs.append(H(ctl.step(T(x), T(rho), T(Uo), cfg)["U"]))
+    assert np.max(np.abs(outs[1] - outs[0])) / 2e6 > 1e-4
+
+
+def test_run_closed_loop_input_weight(ctl):
+    """ntm_mpc_run with Ru > 0 against the C oracle's closed loop (free-running, RUN_TOL)."""
+    B, k_sim = 32, 20
+    cfg, ocfg = cfgs(20, 2, Ru=1e-10)
+    x0 = O.scenario_x0(np.arange(B)).T
+    ref = cbind.run(x0, ocfg, k_sim)
+    out = ctl.run(T(x0), k_sim, cfg)
+    _assert_run_close(out, ref, cfg, k_sim, tol=RUN_TOL, x0=x0, ocfg=ocfg)
 
 
 # N = 20 has two builds (ntm_ctx_set_small_batch): batches up to 32 x the compute
@@ -746,8 +787,9 @@ def test_step_workspace_roundtrip_host(ctl):
 
 
 def test_empty_batch_and_invalid_arguments(ctl):
-    """B = 0 is a no-op; out-of-range N, an unknown mode or a non-finite du_max
-    are API errors (NTM_E_INVALID with a message), not solver outcomes."""
+    """B = 0 is a no-op; out-of-range N, an unknown mode, a non-finite du_max or
+    a negative or non-finite Ru are API errors (NTM_E_INVALID with a message), not
+    solver outcomes."""
     from ntm_mpc import NtmLibraryError
     N = 20
     cfg, _ = cfgs(N, 2)
@@ -756,7 +798,8 @@ def test_empty_batch_and_invalid_arguments(ctl):
     out = ctl.step(x, rho, uo, cfg)
     assert out["U"].shape == (N, 0) and out["exitflag"].shape == (0,)
     x1 = T(O.scenario_x0(np.arange(2)).T)
-    for bad in (dict(N=0), dict(N=65), dict(mode=4), dict(mode=3, du_max=float("nan"))):
+    for bad in (dict(N=0), dict(N=65), dict(mode=4), dict(mode=3, du_max=float("nan")), dict(Ru=-1e-10),
+                dict(Ru=float("nan")), dict(Ru=float("inf"))):
         c = cfgs(bad.pop("N", N), bad.pop("mode", 2), **bad)[0]
         with pytest.raises(NtmLibraryError):
             r, u = ctl.initial_state(x1, c)

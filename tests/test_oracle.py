@@ -234,12 +234,80 @@ def test_qp_golden_certified(name):
             assert np.max(np.abs(U - d["U_exact"][i])) / sc <= 1e-13, (i, np.max(np.abs(U - d["U_exact"][i])) / sc)
 
 
+@pytest.mark.parametrize("name", ["qp_ss_m2_N20", "qp_ss_m3_N50"])
+def test_steady_state_fixture_certified(name):
+    """The steady-state QP fixtures (closed-loop steps 6-25, every
+    inner iteration, NTM_MPC_Sim.m:93-97,123-127) that the GPU test feeds to the
+    fused step kernel: each QP rebuilt from its (x_k, rho) by the oracle's lift /
+    cost / getWLc (NTM_MPC_Sim.m:97,119-121) has U_exact as its KKT point: primal
+    feasible to 1e-12, multipliers >= 0, stationarity G U + F + Lin_A' lam = 0 to
+    1e-9 of |F| (fp64 evaluation of the 50-digit point), and the C oracle solves
+    it to within 1e-13 umax.  The carried warm-start sets are valid active sets."""
+    d = np.load(GOLD / f"{name}.npz")
+    N, mode = int(d["N"]), int(d["mode"])
+    c = cfg(N, mode)
+    for i in range(d["x"].shape[0]):
+        Rho = d["rho"][i].reshape(N, 3).T
+        Phi, Gam, Lam = O.lift(Rho, PH, c)
+        G, F = O.cost(Phi, Gam, Lam, d["x"][i], c)
+        Lin, b = O.constraints(Phi, Gam, Lam, d["x"][i], c)
+        Ue, q = d["U_exact"][i], int(d["act"][i, N])
+        act, lam = d["act"][i, :q], d["lam"][i, :q]
+        nz = np.any(Lin != 0, axis=1)
+        assert np.all((Lin @ Ue - b)[nz] <= 1e-12 * np.maximum(1.0, np.abs(b[nz])))
+        assert np.all(lam >= -1e-12 * max(1.0, np.max(np.abs(lam), initial=0.0)))
+        r = G @ Ue + F + Lin[act].T @ lam
+        assert np.max(np.abs(r)) <= 1e-9 * np.max(np.abs(F)), (i, np.max(np.abs(r)) / np.max(np.abs(F)))
+        Uc, fc, _ = cbind.qp(G, F, Lin, b)
+        assert fc == 1 and np.max(np.abs(Uc - Ue)) / c.umax <= 1e-13, (i, np.max(np.abs(Uc - Ue)) / c.umax)
+        qc = int(d["cand"][i, N])
+        if qc >= 0:
+            ids = d["cand"][i, :qc]
+            assert len(set(ids.tolist())) == qc and ids.min() >= 0 and ids.max() < Lin.shape[0]
+
+
 def test_kkt_certificate_50_digits():
     d = np.load(GOLD / "qp_m2_N20.npz")
     for i in range(3):
         U, flag, info = O.qp_solve(d["G"][i], d["F"][i], d["Lin"][i], d["b"][i])
         Ue, lam, cert = O.kkt_polish(d["G"][i], d["F"][i], d["Lin"][i], d["b"][i], info["active"], dps=50)
         assert cert["max_violation"] <= 1e-12 and cert["min_multiplier"] >= -1e-12
+
+
+def test_input_weight_cost_and_certified_qp():
+    """Input weight R_u (ABI v5; SURVEY §2.1 D17 "Q, R_u exposed in config"; the
+    reference has R_u = 0, NTM_MPC_Sim.m:59,72-73): the cost sum x'Qx + R_u u^2 adds
+    exactly 2 R_u I to G = 2 Gamma' Om Gamma and leaves F alone; Ru = 0 is the
+    reference's cost bit for bit.  The QPs of one closed-loop step with R_u > 0 are
+    solved by both restatements to within 1e-13 umax of the 50-digit KKT point of
+    their active set, which certifies (primal feasible, multipliers >= 0)."""
+    N = 20
+    x = O.scenario_x0([4])[0]
+    c0 = cfg(N, O.MODE_FULL)
+    Rho = O.initial_rho(x, PH, c0)
+    Phi, Gam, Lam = O.lift(Rho, PH, c0)
+    G0, F0 = O.cost(Phi, Gam, Lam, x, c0)
+    assert np.array_equal(G0, 2 * Gam.T @ O.omega_blk(c0) @ Gam)
+    for Ru in (1e-11, 1e-9):
+        c = cfg(N, O.MODE_FULL, Ru=Ru)
+        G, F = O.cost(Phi, Gam, Lam, x, c)
+        assert np.array_equal(G, G0 + 2 * Ru * np.eye(N)) and np.array_equal(F, F0)
+        Lin, b = O.constraints(Phi, Gam, Lam, x, c)
+        U, flag, info = O.qp_solve(G, F, Lin, b)
+        Uc, fc, _ = cbind.qp(G, F, Lin, b)
+        assert flag == fc == 1
+        Ue, lam, cert = O.kkt_polish(G, F, Lin, b, info["active"], dps=50)
+        assert cert["max_violation"] <= 1e-12 and cert["min_multiplier"] >= -1e-12 * max(1.0, np.max(np.abs(lam)))
+        assert np.max(np.abs(U - Ue)) / c.umax <= 1e-13
+        assert np.max(np.abs(Uc - Ue)) / c.umax <= 1e-13
+    # the weight moves the plans of a closed-loop step (this first QP's plan is held
+    # by its active rows alone; the step's later LPV iterations are not)
+    xs = O.scenario_x0(np.arange(8)).T
+    moved = []
+    for Ru in (0.0, 1e-9):
+        c = cfg(N, O.MODE_FULL, Ru=Ru)
+        moved.append(cbind.step(xs, *cbind.initial_state(xs, c), c)["U"])
+    assert np.max(np.abs(moved[1] - moved[0])) / c0.umax > 1e-2
 
 
 def test_unconstrained_lq_vs_mpmath():
