@@ -1002,6 +1002,9 @@ typedef double ntm_d4 __attribute__((ext_vector_type(4)));
 #ifndef NTM_MFMA_FF
 #define NTM_MFMA_FF 0      // the re-solve's compact G~_FF (bordered path): measured slower, off
 #endif
+#ifndef NTM_ROWE_ALL
+#define NTM_ROWE_ALL 0     // 1: the echelon re-solve builds E one sorted row per lane at every horizon
+#endif
 #ifndef NTM_MFMA_FULL
 #define NTM_MFMA_FULL 1    // GI's full G~
 #endif
@@ -2292,10 +2295,17 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     //     next lift) and z = y_B + e - r (scratch in w.xp(), rewritten by the rollout) ---
     NTM_WSYNC();
     NTM_ACC(ST_C_B, tp);
+    // Every variable fixed by a bound (no free variable, no general row: the box-only
+    // QPs of BASELINE config 2 hold 19.8 of 20 inputs at a bound): Gamma U_B is the
+    // certificate's y = Gamma U already, so the pass below writes it where the
+    // certificate reads it and the certificate skips its own Gamma U pass (the
+    // all-LDS and generic builds; the far N = 20 / 50 kernels keep one code path)
+    constexpr bool kFixedY = !W::kFar;
+    const bool allfixed = kFixedY && nF == 0 && nS == 0;
     for (int r = l; r < 2 * N; r += P) {
         const double y = gamma_row_dot<NTM_CH>(w, r, w.dr());
         w.Phi()[r] = y;
-        w.xp()[r] = y + w.e()[r] - ((r & 1) ? pb.r[1] : pb.r[0]);
+        w.xp()[r] = allfixed ? y : y + w.e()[r] - ((r & 1) ? pb.r[1] : pb.r[0]);
     }
     NTM_WSYNC();
     NTM_ACC(ST_C_Y, tp);
@@ -2454,7 +2464,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     int fk = ok ? 0 : 3, fpos_out = 0;
     double vfin = 0.0;
     double sq_id = 0.0;                                   // echelon path: 1 / E_p[t][t] on lane t
-    bool y_ready = false;                                 // k = 1: y = Gamma U already in w.xp()
+    bool y_ready = allfixed;                              // k = 1 / all fixed: y = Gamma U already in w.xp()
     if (sq) {
         // Sorted E over the pivot columns (row t = general row perm[t] ends in pivot
         // column pc(t) = t + (t >= nc); lower triangular, n x n row-major at Lp[t LD + u]),
@@ -2472,7 +2482,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         // address on every lane (broadcast reads), only Gamma_rj differs.  The entry-
         // per-lane loop below issues ~5 dependent loads per entry, n^2 / 64 times per
         // lane (n ~ 43 at N = 50).  Entries as gen_n computes them, bit for bit.
-        constexpr bool kRowE = W::kNN > 32 || W::kNN == 0;
+        constexpr bool kRowE = W::kNN > 32 || W::kNN == 0 || NTM_ROWE_ALL;
         if constexpr (kRowE) {
             if (l < n) {
                 const int s2 = perm[l];
@@ -2957,18 +2967,21 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             ok = vf.p == 0;
         }
         NTM_ACC(ST_K_CHK, tp);
-        // gradient G~V + F~ = D (2 Gamma' Om y) + F~
-        // (y is dead after the primal check: Om y in place, once per stage)
+        // gradient G~V + F~ = D (2 Gamma' Om y) + F~, with Om y once per stage into
+        // scratch (w.Phi() + 2N: Phi is dead until the next lift; the sparse pass
+        // below uses its first nS entries, the refinement its first nt <= 2N): y
+        // itself stays in w.xp(), where the rollout of a certified U reads it
+        double* const omy = w.Phi() + 2 * N;
         if (l < N) {
             const double y0 = w.xp()[2 * l], y1 = w.xp()[2 * l + 1];
-            w.xp()[2 * l] = q00 * y0 + q01 * y1;
-            w.xp()[2 * l + 1] = q10 * y0 + q11 * y1;
+            omy[2 * l] = q00 * y0 + q01 * y1;
+            omy[2 * l + 1] = q10 * y0 + q11 * y1;
         }
         NTM_WSYNC();
         double res = 0.0;
         if (l < N) {
             const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;
-            const double g2 = dot_rows2<NTM_CH>(cl, w.xp(), N, l);   // terms i < l masked
+            const double g2 = dot_rows2<NTM_CH>(cl, omy, N, l);      // terms i < l masked
             double gu = 2 * g2;
             if constexpr (ru_on<W>()) gu = gu + 2 * pb.Ru * w.U()[l];  // + 2 Ru U_l
             res = w.D()[l] * gu + w.F()[l];
@@ -3122,6 +3135,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 }
                 NTM_WSYNC();
                 refine = false;
+                y_ready = false;                           // V moved: y again
                 continue;
             }
         }
@@ -3169,11 +3183,41 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
 // rollout + scheduling update + convergence (NTM_MPC_Sim.m:110-117, 123-127)
 // Returns (group-uniform) whether sum|Uold - U| < eps; updates Uold.
 // ---------------------------------------------------------------------------
+// With y_valid (the QP's U was certified by polish_compact, which leaves y = Gamma U
+// in w.xp()) the rollout is the lifted prediction itself: x^_{i+1} = e_i + (Gamma U)_i
+// with e = Phi x_k + Lambda, one row per lane.  That is the rollout identity the
+// oracle tests pin (CANON D4/D6: Phi x_0 + Gamma U + Lambda == the recursion of
+// NTM_MPC_Sim.m:113 with this iteration's rho), evaluated in another order: the
+// same states to rounding, without the N-step serial recursion.  Otherwise (GI's
+// uncertified result, a non-optimal flag, the literal D4/D6 lifts, for which the
+// identity does not hold) the recursion runs on lane 0 as the reference writes it.
 template <int P, class W>
-__device__ __forceinline__ bool rollout_phase(const Prob& pb, const W& w, double x0, double x1, int l) {
+__device__ __forceinline__ bool rollout_phase(const Prob& pb, const W& w, double x0, double x1, int l,
+                                              bool y_valid = false) {
     const int N = w.n();
     const Coef k = scn_coef(pb, w);
-    if (l == 0) {
+    if constexpr (W::kNN == 0) {
+        if (pb.flags & (NTM_LITERAL_PHI_RIGHTMUL | NTM_LITERAL_GAMMA_INDEX)) y_valid = false;
+    }
+    constexpr int RR = W::kNN > 0 ? (2 * W::kNN + P - 1) / P : 2;   // rows per lane (2N <= 2P)
+    if (y_valid) {
+        double v[RR];
+#pragma unroll
+        for (int t = 0; t < RR; ++t) {
+            const int r = l + t * P;
+            v[t] = (r < 2 * N) ? w.e()[r] + w.xp()[r] : 0.0;
+        }
+        NTM_WSYNC();
+#pragma unroll
+        for (int t = 0; t < RR; ++t) {
+            const int r = l + t * P;
+            if (r < 2 * N) w.xp()[r + 2] = v[t];
+        }
+        if (l == 0) {
+            w.xp()[0] = x0;
+            w.xp()[1] = x1;
+        }
+    } else if (l == 0) {
         double y0 = x0, y1 = x1;
         w.xp()[0] = y0;
         w.xp()[1] = y1;
@@ -3295,8 +3339,9 @@ __device__ __forceinline__ int shifted_into_act(const Prob& pb, const W& w, cons
 template <int P, class W>
 __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, double x1, int l, int* qp_iters,
                         int* q_out, int* ns_out, int slot, int* n_try = nullptr, int* n_girun = nullptr,
-                        int it = 0) {
+                        int it = 0, bool* y_valid = nullptr) {
     const int N = w.n();
+    bool yv = false;                                     // w.xp() holds Gamma U of the final U
     NTM_T0(tq);
     lift_phase<P>(pb, w, l);
     NTM_ACC(ST_LIFT, tq);
@@ -3380,6 +3425,7 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                         flag = NTM_EXIT_OPTIMAL;
                         q = cq;
                         done = true;
+                        yv = true;
                         NTM_CNT(CN_HIT);
                         if (rep > 0) NTM_CNT(CN_REPAIR);
                         break;
@@ -3507,7 +3553,7 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                     if (flag == NTM_EXIT_OPTIMAL) {
                         const bool okp = polish_compact<P>(pb, w, rows, q, l, false, &ns);
                         NTM_TRACE("QP GI flag %d q %d polish %d\n", flag, q, (int)okp);
-                        (void)okp;
+                        yv = okp;
                     }
                     NTM_ACC(ST_POLISH, tq);
                 }
@@ -3529,6 +3575,7 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
 #endif
     if (q_out) *q_out = q;
     if (ns_out) *ns_out = ns;
+    if (y_valid) *y_valid = yv && flag == NTM_EXIT_OPTIMAL;
     return flag;
 }
 

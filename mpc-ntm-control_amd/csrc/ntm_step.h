@@ -84,6 +84,10 @@ __device__ __forceinline__ void load_candidates(const Prob& pb, const W& w, int6
     }
 }
 
+// 1: the rollout of a certified plan is the lifted prediction e + Gamma U (rollout_phase)
+#ifndef NTM_ROLL_LIFTED
+#define NTM_ROLL_LIFTED 1
+#endif
 // one MPC step on LDS-resident state; returns exit flag, sets *iters
 template <int P, class W>
 __device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x0, double x1, int l, int* iters,
@@ -99,13 +103,14 @@ __device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x
 #endif
     for (it = 1; it <= pb.i_sim; ++it) {
         int qi = 0, qa = 0, ns = 0;
-        flag = qp_phase<P>(pb, w, x0, x1, l, &qi, &qa, &ns, (it - 1) & 1, &n_try, &n_girun, it);
+        bool yv = false;
+        flag = qp_phase<P>(pb, w, x0, x1, l, &qi, &qa, &ns, (it - 1) & 1, &n_try, &n_girun, it, &yv);
         ++n_qp;
         n_gi += qi;
         n_act += qa;
         n_gen += ns;
         NTM_T0(tr);
-        bool conv = rollout_phase<P>(pb, w, x0, x1, l);
+        bool conv = rollout_phase<P>(pb, w, x0, x1, l, NTM_ROLL_LIFTED && yv);
         NTM_ACC(ST_ROLL, tr);
 #ifdef NTM_STAMPS
         {

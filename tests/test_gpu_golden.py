@@ -21,11 +21,10 @@ KKT solve).  These pin the HIP path itself, not only the oracle:
 
 Tolerances: QP 1e-10 * umax (north_star's control-sequence bound) against the
 exact optimum; functions 1e-13 relative (Phi/Gamma/Lambda, getWLc) and 1e-12
-of the largest entry (G, F); free-running closed loops RUN_TOL = 5e-8, the
-bound of the C-oracle comparisons (test_gpu_parity.py): the C oracle itself
-reproduces these NumPy fixtures to <= 2.1e-14 umax (uk, Uk), 7.4e-16 (xk,
-wpred) and identical inner iterations (tools/fixture_drift.py), so the bound is
-the loop's amplification of per-step rounding, not the fixture's own spread.
+of the largest entry (G, F); the short free-running closed-loop fixtures 1e-10
+(FIX_TOL): the C oracle itself reproduces these NumPy fixtures to <= 2.1e-14
+umax (uk, Uk), 7.4e-16 (xk, wpred) with identical inner iterations
+(tools/fixture_drift.py), the GPU to <= 6e-13 umax on uk.
 """
 import math
 from pathlib import Path
@@ -51,8 +50,11 @@ def H(t):
     return t.cpu().numpy()
 
 
-# free-running closed loops against the fixtures: the bound of the C-oracle comparisons
-RUN_TOL = 5e-8
+# free-running closed loops against the fixtures (short loops: 4-20 steps, 1-4
+# scenarios): the C oracle reproduces them to <= 2.1e-14 umax (tools/fixture_drift.py)
+# and the GPU measured <= 6e-13 umax on uk (round 5); the bound is north_star's
+# per-step 1e-10 (round 4 held these at 1e-6)
+FIX_TOL = 1e-10
 
 QP_FIXTURES = ["qp_m1_N20", "qp_m2_N20", "qp_m3_N20", "qp_m2_N50", "qp_m3_N50", "qp_m0_N10", "qp_m2_N10"]
 
@@ -154,7 +156,7 @@ def test_run_vs_closed_loop_fixture(ctl, name):
     finally:
         ctl.set_scenarios(None)
     np.testing.assert_array_equal(fl.T, d["exitflag"])
-    tol = RUN_TOL
+    tol = FIX_TOL
     print(f"{name}: |duk| {np.max(np.abs(uk.T - d['uk'])) / cfg.umax:.2e} umax")
     assert np.max(np.abs(uk.T - d["uk"])) <= tol * cfg.umax
     Ukr = Uk.reshape(k_sim, N, S).transpose(2, 1, 0)             # fixture: (S, N, k_sim)

@@ -6,9 +6,10 @@ Tolerances (fp64 everywhere; north_star asks <= 1e-10 relative on U):
   * G, F: 1e-12 relative to the largest entry of the same matrix
   * QP / one MPC step (teacher-forced: identical inputs to the GPU and the
     oracle every step): max |U_gpu - U_oracle| / umax <= 1e-10
-  * free-running closed loop: <= 1e-6 (rounding is amplified by the closed
-    loop; the two CPU oracles themselves diverge by up to ~4e-8 over 20 steps,
-    see DESIGN.md §Parity)
+  * free-running closed loop: RUN_TOL = 5e-8 (rounding is amplified by the
+    closed loop; unconstrained mode 0 1e-6 of umax, its minimisers
+    being unbounded); the 256-scenario loops of test_gpu_parity_wide.py bound
+    each scenario by max(RUN_TOL, 10 x the loop's own sensitivity)
 """
 import dataclasses
 import math
@@ -579,7 +580,8 @@ def test_run_closed_loop(ctl, N, mode):
     """ntm_mpc_run (NTM_MPC_Sim.m:80-131) against the C oracle's closed loop: every
     workspace output north_star names, the applied inputs uk, the plans Uk
     (:106), the states xk and the predicted island width wpred (x_pred's w row,
-    :110-117), free-running (rounding amplified by the loop: 1e-6)."""
+    :110-117), free-running (rounding amplified by the loop: RUN_TOL = 5e-8 in
+    modes 1-3, 1e-6 in mode 0)."""
     B, k_sim = 32, 20
     cfg, ocfg = cfgs(N, mode)
     x0 = O.scenario_x0(np.arange(B)).T if mode else np.tile(O.REFERENCE_X0[:, None], (1, B))

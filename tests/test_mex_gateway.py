@@ -138,6 +138,27 @@ def test_mex_library_errors_surface_as_matlab_errors(mex):
 
 # ---------------------------------------------------------------- GPU: bit-identical to ctypes
 @pytest.mark.gpu
+def test_mex_input_weight_field(mex, ctl):
+    """cfg.Ru (ABI v5, the input weight) reaches the library through the gateway: a
+    'step' with Ru = 1e-10 equals the ctypes call with the same Config, bit for bit,
+    and differs from the Ru = 0 step."""
+    from ntm_mpc import Config, scenarios_x0
+    B, N = 8, 20
+    x0 = np.ascontiguousarray(scenarios_x0(0, B))
+    outs = []
+    for Ru in (1e-10, 0.0):
+        mcfg = {"N": float(N), "mode": 2.0, "Ru": Ru}
+        cfg = Config(N=N, mode=2, Ru=Ru)
+        rho_m, uo_m = mex("init", x0, mcfg, nout=2)
+        rho_h, uo_h = ctl.initial_state_host(x0, cfg)
+        U = mex("step", x0, rho_m, uo_m, mcfg, nout=1)[0]
+        h = ctl.step_host(x0, rho_h, uo_h, cfg)
+        np.testing.assert_array_equal(U, h["U"])
+        outs.append(U)
+    assert np.max(np.abs(outs[0] - outs[1])) > 0
+
+
+@pytest.mark.gpu
 def test_mex_matches_ctypes_path(mex, ctl):
     """'init' / 'step' (warm-start workspace carried) / 'run' / 'scenarios'
     through the gateway == the same calls through ctypes, bit for bit, with a
@@ -149,7 +170,7 @@ def test_mex_matches_ctypes_path(mex, ctl):
     Qm = np.array([[2.0e4, 3.0], [3.0, 2.0e-2]])
     mcfg = {"N": float(N), "i_sim": 10.0, "mode": 2.0, "flags": 0.0, "Ts": 0.1, "xmin": [0.06, 200 * np.pi],
             "xmax": [0.15, 10000 * np.pi], "umin": 0.0, "umax": 2e6, "Q": Qm, "r": [0.09, 1800 * np.pi],
-            "epsilon": 1e-14, "du_max": 5e5}
+            "epsilon": 1e-14, "du_max": 5e5, "Ru": 0.0}
     cfg = Config(N=N, mode=2, Q=tuple(Qm.reshape(-1)), r=(0.09, 1800 * np.pi))
     x0 = np.ascontiguousarray(scenarios_x0(0, B))
     rho_m, uo_m = mex("init", x0, mcfg, nout=2)
