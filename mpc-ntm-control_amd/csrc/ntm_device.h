@@ -423,6 +423,9 @@ __device__ __forceinline__ double coef_b(const Coef& k, double r3) { return k.bc
 #ifndef NTM_FAR_JB
 #define NTM_FAR_JB 0         // columns per trip of the bordered elimination's loads in the far block (0: two, loaded as used)
 #endif
+#ifndef NTM_GI_LDS
+#define NTM_GI_LDS 0         // far layouts: GI's G~ / L (bit 0) and R (bit 1) in the LDS E block (WS::gr)
+#endif
 #ifndef NTM_FAR_COLMAJOR
 #define NTM_FAR_COLMAJOR 0   // 1: J, T and the bordered factor column-major in the far block (slower)
 #endif
@@ -496,6 +499,41 @@ struct WS {
         return kCol ? c * (nt + 1) - (c * (c - 1)) / 2 - c : c;
     }
     // echelon re-solve: sorted E (entry (t, u), u <= t, at Ep()[eidx(t, u)]) and the
+    // GI's triangular factor R (and, before it, the scaled Gram G~ and its Cholesky
+    // factor L): element (i, j) at R()[i + j ldj()], or, in the far layouts
+    // (kGiLds), in the LDS E block, which is dead while GI runs (the echelon
+    // re-solve's sorted E is rebuilt by every re-solve): the lower triangle row-major
+    // packed (row i at i(i+1)/2, so G~ / L rows are contiguous), the upper triangle
+    // column-major packed in the same slots ((i, j) and (j, i) share one: the lower
+    // triangle is dead once R is being built, the factor below R's subdiagonal is
+    // never touched), and R's superdiagonal (i, i+1) apart after the triangle, so
+    // that a drop's upper-Hessenberg subdiagonal (i+1, i) does not collide with it.
+    // N(N+1)/2 + N-1 doubles <= the E block's N(N+1)/2 + N+1.  GI's back and forward
+    // substitutions, adds and drops then run on LDS instead of the HBM far block
+    // (J stays there)
+    // (NTM_GI_LDS bit 0: G~ and L, bit 1: R; the two phases never overlap, so each
+    // may live in either place)
+    static constexpr bool kGiLdsL = FAR && (NTM_GI_LDS & 1);
+    static constexpr bool kGiLds = FAR && (NTM_GI_LDS & 2);
+    __device__ __forceinline__ int gio(int i, int j) const {
+        if (i >= j) return (i * (i + 1)) / 2 + j;
+        if (i == j - 1) return (n() * (n() + 1)) / 2 + i;
+        return (j * (j + 1)) / 2 + i;
+    }
+    __device__ __forceinline__ double& gr(int i, int j) const {
+        if constexpr (kGiLds) return Ep()[gio(i, j)];
+        else return R()[i + j * ldj()];
+    }
+    __device__ __forceinline__ double& grL(int i, int j) const {   // lower triangle, i >= j
+        if constexpr (kGiLdsL) return Ep()[(i * (i + 1)) / 2 + j];
+        else return R()[i + j * ldj()];
+    }
+    // row i of the lower triangle (elements (i, 0..i) at stride grs())
+    __device__ __forceinline__ double* grow(int i) const {
+        if constexpr (kGiLdsL) return Ep() + (i * (i + 1)) / 2;
+        else return R() + i;
+    }
+    __device__ __forceinline__ int grs() const { return kGiLdsL ? 1 : ldj(); }
     // row permutation / column owner ints (2(N+1)); in the J/R block unless kFar
     __device__ __forceinline__ double* Ep() const {
         if constexpr (kFar) return base + oJ();
@@ -1065,11 +1103,11 @@ __device__ __forceinline__ void gram_mfma(const Prob& pb, const W& w, int nc, Co
 // condensed cost G = 2 Gamma' Om Gamma (lower triangle into dst, col-major),
 // F = 2 Gamma' Om (e - R)      NTM_MPC_Sim.m:120-121 (CANON D8, D12)
 // ---------------------------------------------------------------------------
-template <int P, class W>
-__device__ __forceinline__ void gram_rows(const Prob& pb, const W& w, double* dst, int l) {
-    const int N = w.n(), LD = w.ldj();
+template <int P, class W, class Put>
+__device__ __forceinline__ void gram_rows_put(const Prob& pb, const W& w, Put put, int l) {
+    const int N = w.n();
     if constexpr (NTM_MFMA_FULL && W::kNN > 32 && P == 64) {   // the matrix cores (gram_mfma)
-        gram_mfma<W::kNN>(pb, w, N, [](int a) { return a; }, [&](int j, int kk, double sg) { dst[j + kk * LD] = 2 * sg; },
+        gram_mfma<W::kNN>(pb, w, N, [](int a) { return a; }, [&](int j, int kk, double sg) { put(j, kk, 2 * sg); },
                           l);
         return;
     }
@@ -1094,8 +1132,13 @@ __device__ __forceinline__ void gram_rows(const Prob& pb, const W& w, double* ds
         }
         double gv = 2 * s;
         if constexpr (ru_on<W>()) gv = (j == kk) ? gv + 2 * pb.Ru : gv;   // + 2 Ru I (ABI v5)
-        dst[j + kk * LD] = gv;      // G(j, kk), j >= kk
+        put(j, kk, gv);             // G(j, kk), j >= kk
     }
+}
+template <int P, class W>
+__device__ __forceinline__ void gram_rows(const Prob& pb, const W& w, double* dst, int l) {
+    const int LD = w.ldj();
+    gram_rows_put<P>(pb, w, [&](int j, int kk, double v) { dst[j + kk * LD] = v; }, l);
 }
 
 template <int P, class W>
@@ -1234,12 +1277,26 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
     return ok;
 }
 
-// the full scaled Hessian G~ (lower, col-major) into w.R() for the GI fallback
+// the full scaled Hessian G~ (lower triangle, WS::gr) for the GI fallback
 template <int P, class W>
 __device__ __forceinline__ bool full_gram(const Prob& pb, const W& w, int l) {
-    gram_rows<P>(pb, w, w.R(), l);
-    NTM_WSYNC();
-    int bad = scale_gram<P>(w, w.R(), l);
+    int bad = 0;
+    if constexpr (W::kGiLdsL) {
+        gram_rows_put<P>(pb, w, [&](int j, int kk, double v) { w.grL(j, kk) = v; }, l);
+        NTM_WSYNC();
+        if (l < w.n()) {                      // scale_gram's expression order
+            const double Dl = w.D()[l];
+            for (int kk = 0; kk <= l; ++kk) {
+                const double v = w.grL(l, kk) * Dl * w.D()[kk];
+                bad |= !isfinite(v);
+                w.grL(l, kk) = v;
+            }
+        }
+    } else {
+        gram_rows<P>(pb, w, w.R(), l);
+        NTM_WSYNC();
+        bad = scale_gram<P>(w, w.R(), l);
+    }
     NTM_WSYNC();
     return gmaxi<P>(bad) == 0;
 }
@@ -1564,6 +1621,26 @@ __device__ __forceinline__ bool chol_inplace(double* A, int n, int RS, int CS, i
     }
     return true;
 }
+// chol_inplace on GI's factor storage (WS::gr / grow: rows of the lower triangle)
+template <int P, class W>
+__device__ __forceinline__ bool chol_gr(const W& w, int n, int l, double* rdiag) {
+    if constexpr (!W::kGiLdsL) {
+        return chol_inplace<P>(w.R(), n, 1, w.ldj(), l, rdiag);
+    } else {
+        for (int k = 0; k < n; ++k) {
+            double s = 0.0;
+            if (l >= k && l < n) s = sub_dot<NTM_CH>(w.grL(l, k), w.grow(l), 1, w.grow(k), 1, 0, k);
+            const double dk = gbcast<P>(s, k);
+            if (!(dk > 0.0) || !(dk < kInf)) return false;
+            const double il = rsqrt_nr(dk);
+            const double lk = dk * il;
+            if (l > k && l < n) w.grL(l, k) = s * il;
+            if (l == k) { w.grL(k, k) = lk; rdiag[k] = il; }
+            NTM_WSYNC();
+        }
+        return true;
+    }
+}
 // lane i holds b_i in `v`; returns x_i of L x = b (L lower, rdiag = 1/diag)
 template <int P>
 __device__ __forceinline__ double fwd_lanes(const double* L, const double* rdiag, int n, int RS, int CS, double v, int l) {
@@ -1605,13 +1682,13 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
     *q_out = 0;
     NTM_T0(tg);
     // 1. Cholesky G~ = L L' (in place in w.R())
-    if (!chol_inplace<P>(w.R(), N, 1, LD, l, w.ldi())) return NTM_EXIT_NONFINITE;
+    if (!chol_gr<P>(w, N, l, w.ldi())) return NTM_EXIT_NONFINITE;
     // 2. J = L^{-T}: lane c computes row c of J (= column c of L^{-1})
     if (l < N) {
         for (int i = 0; i < N; ++i) {
             double x = 0.0;
             if (i >= l) {
-                x = sub_dot<NTM_CH>((i == l) ? 1.0 : 0.0, w.R() + i, LD, w.J() + l * JR, JC, l, i);
+                x = sub_dot<NTM_CH>((i == l) ? 1.0 : 0.0, w.grow(i), w.grs(), w.J() + l * JR, JC, l, i);
                 x *= w.ldi()[i];
             }
             w.J()[l * JR + i * JC] = x;
@@ -1697,11 +1774,11 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
             }
             const double ih = 1.0 / h;
             if (l < q) {
-                w.R()[l + q * LD] = dl;
+                w.gr(l, q) = dl;
                 if (useT) w.T()[l * JR + q * JC] = -rl * ih;
             }
             if (l == q) {
-                w.R()[q + q * LD] = h;
+                w.gr(q, q) = h;
                 if (useT) w.T()[q * JR + q * JC] = ih;
                 w.act()[q] = p;
                 w.aflag()[p] = kActiveRow;
@@ -1719,9 +1796,9 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
             } else {                                 // long horizons: R' wv = bc by forward substitution
                 double acc = (l < q) ? w.Vb()[l] : 0.0;
                 for (int k2 = 0; k2 < q; ++k2) {
-                    const double xk = gbcast<P>(acc, k2) / w.R()[k2 + k2 * LD];
+                    const double xk = gbcast<P>(acc, k2) / w.gr(k2, k2);
                     if (l == k2) wv = xk;
-                    if (l > k2 && l < q) acc -= w.R()[k2 + l * LD] * xk;
+                    if (l > k2 && l < q) acc -= w.gr(k2, l) * xk;
                 }
             }
             if (l < N) {
@@ -1737,9 +1814,9 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
             } else {                                 // R u = wv + c1 by back substitution
                 double acc = (l < q) ? w.np()[l] : 0.0;
                 for (int b = q - 1; b >= 0; --b) {
-                    const double ub = gbcast<P>(acc, b) / w.R()[b + b * LD];
+                    const double ub = gbcast<P>(acc, b) / w.gr(b, b);
                     if (l == b) u = ub;
-                    if (l < b) acc -= w.R()[l + b * LD] * ub;
+                    if (l < b) acc -= w.gr(l, b) * ub;
                 }
             }
             const double uabs = gmax<P>(l < q ? fabs(u) : 0.0);
@@ -1815,9 +1892,9 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
             if (!useT) {                       // long horizons: back substitution on R
                 double acc = (l < q) ? dl : 0.0;
                 for (int b = q - 1; b >= 0; --b) {
-                    const double rb = gbcast<P>(acc, b) / w.R()[b + b * LD];
+                    const double rb = gbcast<P>(acc, b) / w.gr(b, b);
                     if (l == b) rl = rb;
-                    if (l < b) acc -= w.R()[l + b * LD] * rb;
+                    if (l < b) acc -= w.gr(l, b) * rb;
                 }
             }
             // partial (dual) step length t1
@@ -1863,11 +1940,11 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
                     // R gains column q = [d1; h]; T = R^{-1} gains column q = [-r/h; 1/h]
                     const double ih = 1.0 / h;
                     if (l < q) {
-                        w.R()[l + q * LD] = dl;
+                        w.gr(l, q) = dl;
                         if (useT) w.T()[l * JR + q * JC] = -rl * ih;
                     }
                     if (l == q) {
-                        w.R()[q + q * LD] = h;
+                        w.gr(q, q) = h;
                         if (useT) w.T()[q * JR + q * JC] = ih;
                         w.act()[q] = p;
                         w.aflag()[p] = kActiveRow;
@@ -1884,8 +1961,12 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
             const int dropped = uni<P>(w.act()[l0]);
             NTM_WSYNC();
             if (l < q) {
-                for (int c = l0; c < q - 1; ++c) w.R()[l + c * LD] = w.R()[l + (c + 1) * LD];
-                w.R()[l + (q - 1) * LD] = 0.0;
+                // column shift: rows l <= c + 1 (R upper, plus the subdiagonal the shift
+                // creates); the rows below are zero and, in the packed LDS storage
+                // (kGiLds), share their slots with the upper triangle
+                for (int c = l0; c < q - 1; ++c)
+                    if (!W::kGiLds || l <= c + 1) w.gr(l, c) = w.gr(l, c + 1);
+                w.gr(l, q - 1) = 0.0;
             }
             {
                 int an = 0;
@@ -1897,16 +1978,16 @@ __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_ro
             }
             NTM_WSYNC();
             for (int j = l0; j < q - 1; ++j) {
-                double a = uni<P>(w.R()[j + j * LD]), bq = uni<P>(w.R()[(j + 1) + j * LD]);
+                double a = uni<P>(w.gr(j, j)), bq = uni<P>(w.gr(j + 1, j));
                 double hh = hypot(a, bq);
                 double cc = 1.0, ss = 0.0;
                 if (hh != 0.0) { cc = a / hh; ss = bq / hh; }
                 NTM_WSYNC();
                 if (l >= j && l < q - 1) {
-                    double r1 = w.R()[j + l * LD], r2 = w.R()[(j + 1) + l * LD];
+                    double r1 = w.gr(j, l), r2 = w.gr(j + 1, l);
                     double nr = cc * r1 + ss * r2;
-                    w.R()[j + l * LD] = nr;
-                    w.R()[(j + 1) + l * LD] = (l == j) ? 0.0 : (-ss * r1 + cc * r2);
+                    w.gr(j, l) = nr;
+                    w.gr(j + 1, l) = (l == j) ? 0.0 : (-ss * r1 + cc * r2);
                 }
                 if (l < N) {
                     double j1 = w.J()[l * JR + j * JC], j2 = w.J()[l * JR + (j + 1) * JC];

@@ -1,5 +1,8 @@
 """Diagnostic (not a test): per-phase cycle breakdown of the fused step kernel
-using the -DNTM_STAMPS build (lib/libntm_mpc_diag.so)."""
+using the -DNTM_STAMPS build (lib/libntm_mpc_diag.so).
+
+    python tools/diag_phases.py [B] [N] [mode] [warm steps] [measured steps]
+"""
 import ctypes as C, os, sys, time
 os.environ.setdefault("NTM_MPC_LIB", os.path.join(os.path.dirname(__file__), "..", "mpc-ntm-control_amd", "lib", "libntm_mpc_diag.so"))
 sys.path[:0] = [os.path.join(os.path.dirname(__file__), ".."), os.path.join(os.path.dirname(__file__), "..", "mpc-ntm-control_amd")]
@@ -18,14 +21,18 @@ WARM = int(sys.argv[4]) if len(sys.argv) > 4 else 6   # steps before the measure
 for _ in range(WARM):
     out = ctl.step(x, rho, uo, cfg, active_ws=ws); torch.cuda.synchronize()
     x = out["x_next"].clone()
+K = int(sys.argv[5]) if len(sys.argv) > 5 else 1      # measured steps (bench: 20, steps 6-25)
 lib.ntm_debug_stamps(buf, 1)
 t = time.time()
-out = ctl.step(x, rho, uo, cfg, active_ws=ws); torch.cuda.synchronize()
-dt = time.time() - t
+for _ in range(K):
+    out = ctl.step(x, rho, uo, cfg, active_ws=ws); torch.cuda.synchronize()
+    x = out["x_next"].clone()
+dt = (time.time() - t) / K
 assert lib.ntm_debug_stamps(buf, 1) == 0
+B = B * K                                               # every figure below is per wave-step
 names = "lift cost scale cand regram gi polish roll gi_fact gi_check gi_dir gi_add gi_drop".split()
 tot = sum(buf[i] for i in range(8))
-print(f"B={B} N={N} step {WARM + 1} {dt*1e3:.1f} ms; cycles per wave-step by phase (s_memtime):")
+print(f"B={B // K} N={N} steps {WARM + 1}-{WARM + K} {dt*1e3:.1f} ms; cycles per wave-step by phase (s_memtime):")
 for i, n in enumerate(names):
     print(f"  {n:9s} {buf[i]/B:12.0f}  {100*buf[i]/tot:5.1f}%")
 print(f"per wave-step: check calls {buf[13]/B:.1f}, candidate sets {buf[14]/B:.2f}, hits {buf[15]/B:.2f} (after repair {buf[22]/B:.2f}), GI solves {buf[23]/B:.2f}")
