@@ -424,7 +424,7 @@ __device__ __forceinline__ double coef_b(const Coef& k, double r3) { return k.bc
 #define NTM_FAR_JB 0         // columns per trip of the bordered elimination's loads in the far block (0: two, loaded as used)
 #endif
 #ifndef NTM_GI_LDS
-#define NTM_GI_LDS 0         // far layouts: GI's G~ / L (bit 0) and R (bit 1) in the LDS E block (WS::gr)
+#define NTM_GI_LDS 3         // far layouts: GI's G~ / L (bit 0) and R (bit 1) in the LDS E block (WS::gr)
 #endif
 #ifndef NTM_FAR_COLMAJOR
 #define NTM_FAR_COLMAJOR 0   // 1: J, T and the bordered factor column-major in the far block (slower)
