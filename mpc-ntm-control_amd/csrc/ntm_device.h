@@ -630,6 +630,33 @@ __device__ __forceinline__ double ru_of(const Prob& pb) {
     if constexpr (ru_on<W>()) return pb.Ru;
     else return 0.0;
 }
+// The reference's stage weight is Q = I (NTM_MPC_Sim.m:59, Omega = blkdiag(Q, ...)).
+// The specialised kernels (compile-time horizons) assume it, so their Om products
+// are the identity (bit for bit what 1 x + 0 y gives for finite data) and the
+// weight's four launch constants leave their scalar registers; a launch with any
+// other Q runs on the generic kernels (host dispatch, like Ru and D4 / D6).
+#ifndef NTM_QI_MAXN
+#define NTM_QI_MAXN 32     // compile-time horizons up to this one assume Q = I (qi_on): N = 10, 20 (at
+                           // N = 50 it cost 11% through register allocation, A/B on one box)
+#endif
+template <class W>
+__device__ __forceinline__ constexpr bool qi_on() { return W::kNN > 0 && NTM_QI_MAXN >= W::kNN; }
+template <bool QI>
+struct OmQ {                       // x -> Q x for one stage's 2-vector
+    double q00, q01, q10, q11;
+    __device__ __forceinline__ explicit OmQ(const double* Q) {
+        if constexpr (QI) { q00 = 1.0; q01 = 0.0; q10 = 0.0; q11 = 1.0; }
+        else { q00 = Q[0]; q01 = Q[1]; q10 = Q[2]; q11 = Q[3]; }
+    }
+    __device__ __forceinline__ double o0(double x0, double x1) const {
+        if constexpr (QI) return x0;
+        else return q00 * x0 + q01 * x1;
+    }
+    __device__ __forceinline__ double o1(double x0, double x1) const {
+        if constexpr (QI) return x1;
+        else return q10 * x0 + q11 * x1;
+    }
+};
 __device__ __forceinline__ bool gen_phys(const Prob& pb) { return pb.g.phys_on != 0; }
 __device__ __forceinline__ bool gen_dist(const Prob& pb) { return pb.g.dist_on != 0; }
 template <class W>
@@ -662,9 +689,8 @@ __device__ __forceinline__ void scn_store(const Prob& pb, const W& w, int64_t gi
 // tail chunk past n are skipped (zero), never read out of the workspace.
 // ---------------------------------------------------------------------------
 // sum_{imin <= i < n} a_i' Q b_i over 2-vectors stored at stride 2
-template <int CH>
-__device__ __forceinline__ double qdot_rows(const double* a, const double* b, int n, int imin, double q00,
-                                            double q01, double q10, double q11) {
+template <int CH, class OM>
+__device__ __forceinline__ double qdot_rows(const double* a, const double* b, int n, int imin, const OM& om) {
     double s = 0.0;
     NTM_CHUNK_PRAGMA
     for (int i0 = 0; i0 < n; i0 += CH) {
@@ -682,8 +708,8 @@ __device__ __forceinline__ double qdot_rows(const double* a, const double* b, in
 #pragma unroll
         for (int u = 0; u < CH; ++u) {
             const int i = i0 + u;
-            const double o0 = q00 * b0[u] + q01 * b1[u];
-            const double o1 = q10 * b0[u] + q11 * b1[u];
+            const double o0 = om.o0(b0[u], b1[u]);
+            const double o1 = om.o1(b0[u], b1[u]);
             const double t = a0[u] * o0 + a1[u] * o1;
             s += (i >= imin && i < n) ? t : 0.0;
         }
@@ -989,8 +1015,9 @@ __device__ __forceinline__ void free_response(const W& w, double x0, double x1, 
             // Om (e_i - r) per stage for the scaling pass's F (scratch in w.xp(): the
             // rollout consumed it and rewrites it; the re-solve recomputes it)
             const double d0 = e0 - pw->r[0], d1 = e1 - pw->r[1];
-            w.xp()[2 * i] = pw->Q[0] * d0 + pw->Q[1] * d1;
-            w.xp()[2 * i + 1] = pw->Q[2] * d0 + pw->Q[3] * d1;
+            const OmQ<qi_on<W>()> om(pw->Q);
+            w.xp()[2 * i] = om.o0(d0, d1);
+            w.xp()[2 * i + 1] = om.o1(d0, d1);
         }
     }
     NTM_WSYNC();
@@ -1051,7 +1078,7 @@ __device__ __forceinline__ void gram_mfma(const Prob& pb, const W& w, int nc, Co
     static_assert(NN > 0 && NN % 2 == 0, "gram_mfma: compile-time even horizon");
     constexpr int TM = (NN + 15) / 16;                 // tiles of 16 columns
     constexpr int NP = TM * (TM + 1) / 2;              // lower tile pairs
-    const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
+    const OmQ<qi_on<W>()> om(pb.Q);
     const int li = l & 15, lk = l >> 4;
     const int T = (nc + 15) >> 4;
     int base[TM], r0[TM];
@@ -1076,7 +1103,7 @@ __device__ __forceinline__ void gram_mfma(const Prob& pb, const W& w, int nc, Co
             const bool in = re >= r0[t];
             const double x0 = in ? G[base[t] + re] : 0.0, x1 = in ? G[base[t] + re + 1] : 0.0;
             xa[t] = (lk & 1) ? x1 : x0;
-            yb[t] = (lk & 1) ? (q10 * x0 + q11 * x1) : (q00 * x0 + q01 * x1);
+            yb[t] = (lk & 1) ? om.o1(x0, x1) : om.o0(x0, x1);
         }
         int p = 0;
 #pragma unroll
@@ -1111,7 +1138,7 @@ __device__ __forceinline__ void gram_rows_put(const Prob& pb, const W& w, Put pu
                           l);
         return;
     }
-    const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
+    const OmQ<qi_on<W>()> om(pb.Q);
     // one (j, kk) entry per lane; fixed-trip masked dot (column reads below the
     // packed column start stay inside Gt, see StructRows::check)
     const int npair = N * (N + 1) / 2;
@@ -1125,8 +1152,8 @@ __device__ __forceinline__ void gram_rows_put(const Prob& pb, const W& w, Put pu
         double s = 0.0;
         for (int i = 0; i < N; ++i) {
             const double g0 = ck[2 * i], g1 = ck[2 * i + 1];
-            const double o0 = q00 * g0 + q01 * g1;
-            const double o1 = q10 * g0 + q11 * g1;
+            const double o0 = om.o0(g0, g1);
+            const double o1 = om.o1(g0, g1);
             const double t = cj[2 * i] * o0 + cj[2 * i + 1] * o1;
             s += (i >= j) ? t : 0.0;
         }
@@ -1187,7 +1214,7 @@ __device__ __forceinline__ int scale_gram(const W& w, double* G, int l) {
 template <int P, class W>
 __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_state_rows) {
     const int N = w.n();
-    const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
+    const OmQ<qi_on<W>()> qw(pb.Q);
     int bad = 0;
     NTM_T0(tsc);
     if (l < N) {
@@ -1213,8 +1240,8 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
             for (int u = 0; u < CH; ++u) {
                 const int i = i0 + u;
                 const double g0 = ga[u], g1 = gb[u];
-                const double o0 = q00 * g0 + q01 * g1;
-                const double o1 = q10 * g0 + q11 * g1;
+                const double o0 = qw.o0(g0, g1);
+                const double o1 = qw.o1(g0, g1);
                 const double t = g0 * o0 + g1 * o1;
                 const double tf = g0 * ea[u] + g1 * eb[u];
                 const bool on = i >= l && i < N;
@@ -2292,7 +2319,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                                int* ns_out, int* fail_kind = nullptr, int* fail_pos = nullptr,
                                double* v_out = nullptr) {
     const int N = w.n(), LD = w.ldj(), LDJ = w.ldj();
-    const double q00 = pb.Q[0], q01 = pb.Q[1], q10 = pb.Q[2], q11 = pb.Q[3];
+    const OmQ<qi_on<W>()> om(pb.Q);
     const double Vprev = (l < N) ? w.V()[l] : 0.0;
     NTM_T0(tp);
     // --- classify active rows: single-entry rows fix a variable, the rest are general ---
@@ -2462,7 +2489,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     if (!sq && l < nF) {
         const int ja = w.fidx()[l];
         const double* ca = w.Gt() + w.gidx(2 * ja, ja) - 2 * ja;   // ca[r] = gt(r, ja), r >= 2 ja
-        const double g2 = qdot_rows<NTM_CH>(ca, w.xp(), N, ja, q00, q01, q10, q11);   // terms i < ja masked
+        const double g2 = qdot_rows<NTM_CH>(ca, w.xp(), N, ja, om);   // terms i < ja masked
         gl = w.D()[ja] * (2 * g2);
     }
     // Bordered KKT system (fused path): rows 0..nF-1 free variables, nF..nt-1 general
@@ -2499,7 +2526,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             const int ja = w.fidx()[a], jc = w.fidx()[c];            // ja >= jc
             const double* ca = w.Gt() + w.gidx(2 * ja, ja) - 2 * ja;
             const double* cc = w.Gt() + w.gidx(2 * jc, jc) - 2 * jc;
-            const double sg = qdot_rows<NTM_CH>(ca, cc, N, ja, q00, q01, q10, q11);   // terms i < ja masked
+            const double sg = qdot_rows<NTM_CH>(ca, cc, N, ja, om);   // terms i < ja masked
             double g2v = 2 * sg;
             if constexpr (ru_on<W>()) g2v = (a == c) ? g2v + 2 * pb.Ru : g2v;      // + 2 Ru I
             const double gv = g2v * w.D()[ja] * w.D()[jc];
@@ -2704,7 +2731,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 const double y0a = w.xp()[2 * l] + w.e()[2 * l] - pb.r[0];
                 const double y0b = w.xp()[2 * l + 1] + w.e()[2 * l + 1] - pb.r[1];
                 const double za = w.Phi()[2 * l], zb = w.Phi()[2 * l + 1];
-                const double oa = q00 * za + q01 * zb, ob = q10 * za + q11 * zb;
+                const double oa = om.o0(za, zb), ob = om.o1(za, zb);
                 num = oa * y0a + ob * y0b;
                 den = oa * za + ob * zb;
                 if constexpr (ru_on<W>()) {               // Ru (dU' U_0, dU' dU): w.U() = D V_0, w.d() = D Z
@@ -3055,8 +3082,8 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         double* const omy = w.Phi() + 2 * N;
         if (l < N) {
             const double y0 = w.xp()[2 * l], y1 = w.xp()[2 * l + 1];
-            omy[2 * l] = q00 * y0 + q01 * y1;
-            omy[2 * l + 1] = q10 * y0 + q11 * y1;
+            omy[2 * l] = om.o0(y0, y1);
+            omy[2 * l + 1] = om.o1(y0, y1);
         }
         NTM_WSYNC();
         double res = 0.0;
@@ -3415,6 +3442,57 @@ __device__ __forceinline__ int shifted_into_act(const Prob& pb, const W& w, cons
 }
 
 // ---------------------------------------------------------------------------
+// qp_phase's Goldfarb-Idnani fallback (the full G~, GI warm-started from the
+// failed candidate, then its certified polish; ~2.5% of the QPs at N = 20).
+// NTM_GI_OUTLINE=1 makes it a real call, so that its register allocation is its
+// own instead of the step kernel's (the caller's live registers are saved around
+// the call); 0 inlines it like every other phase.
+// ---------------------------------------------------------------------------
+#ifndef NTM_GI_OUTLINE
+#define NTM_GI_OUTLINE 0
+#endif
+#if NTM_GI_OUTLINE
+#define NTM_GI_ATTR __attribute__((noinline))
+#else
+#define NTM_GI_ATTR __forceinline__
+#endif
+template <int P, class W>
+__device__ NTM_GI_ATTR int gi_fallback(const Prob& pb, const W w, const StructRows rows, int nrows, int l, int nwarm,
+                                       int it, int* qp_iters, int* q_out, int* ns_out, bool* yv_out) {
+    NTM_T0(tq);
+    int flag, q = 0, ns = 0;
+    bool yv = false;
+    if (!full_gram<P>(pb, w, l)) {
+        flag = NTM_EXIT_NONFINITE;
+    } else {
+        NTM_ACC(ST_REGRAM, tq);
+        NTM_CNT(CN_GIRUN);
+        if (it == 1) NTM_CNT(CN_GI_IT1); else if (it == 2) NTM_CNT(CN_GI_IT2); else NTM_CNT(CN_GI_LATE);
+        // warm from the failed candidate; if its multipliers are not all >= 0, warm
+        // again from the rows whose multipliers were; then cold
+        for (int pass = 0;; ++pass) {
+            flag = gi_solve<P, StructRows, W>(w, rows, pb.mode != NTM_MODE_NONE, nrows, l, qp_iters, &q,
+                                              pass < 2 ? nwarm : 0);
+            if (flag != kGiWarmRejected) break;
+            nwarm = (pass == 0) ? q : 0;
+            q = 0;
+            if (!full_gram<P>(pb, w, l)) { flag = NTM_EXIT_NONFINITE; break; }
+        }
+        NTM_ACC(ST_GI, tq);
+        if (flag == NTM_EXIT_OPTIMAL) {
+            const bool okp = polish_compact<P>(pb, w, rows, q, l, false, &ns);
+            NTM_TRACE("QP GI flag %d q %d polish %d\n", flag, q, (int)okp);
+            yv = okp;
+        }
+        NTM_ACC(ST_POLISH, tq);
+    }
+    *q_out = q;
+    *ns_out = ns;
+    *yv_out = yv;
+    return flag;
+}
+
+// ---------------------------------------------------------------------------
 // one inner iteration's QP: build -> scale -> GI -> polish -> w.U()
 // ---------------------------------------------------------------------------
 template <int P, class W>
@@ -3613,31 +3691,8 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                 NTM_ACC(ST_CAND, tq);
             }
             if (!done) {
-                if (!full_gram<P>(pb, w, l)) {
-                    flag = NTM_EXIT_NONFINITE;
-                } else {
-                    NTM_ACC(ST_REGRAM, tq);
-                    if (n_girun) ++*n_girun;
-                    NTM_CNT(CN_GIRUN);
-                    if (it == 1) NTM_CNT(CN_GI_IT1); else if (it == 2) NTM_CNT(CN_GI_IT2); else NTM_CNT(CN_GI_LATE);
-                    // one inlined GI: warm from the failed candidate; if its multipliers are
-                    // not all >= 0, warm again from the rows whose multipliers were; then cold
-                    for (int pass = 0;; ++pass) {
-                        flag = gi_solve<P, StructRows, W>(w, rows, pb.mode != NTM_MODE_NONE, nrows, l,
-                                                          qp_iters, &q, pass < 2 ? nwarm : 0);
-                        if (flag != kGiWarmRejected) break;
-                        nwarm = (pass == 0) ? q : 0;
-                        q = 0;
-                        if (!full_gram<P>(pb, w, l)) { flag = NTM_EXIT_NONFINITE; break; }
-                    }
-                    NTM_ACC(ST_GI, tq);
-                    if (flag == NTM_EXIT_OPTIMAL) {
-                        const bool okp = polish_compact<P>(pb, w, rows, q, l, false, &ns);
-                        NTM_TRACE("QP GI flag %d q %d polish %d\n", flag, q, (int)okp);
-                        yv = okp;
-                    }
-                    NTM_ACC(ST_POLISH, tq);
-                }
+                if (n_girun) ++*n_girun;
+                flag = gi_fallback<P, W>(pb, w, rows, nrows, l, nwarm, it, qp_iters, &q, &ns, &yv);
             }
         }
     }

@@ -611,10 +611,13 @@ bool force_generic() {
 // act almost alike) and sat up to ~1e-8 umax off the exact optimum; compiled into
 // the N = 20 kernel the paths cost mode 2 ~1% through register allocation.
 // The input weight Ru (ABI v5) is compiled into the generic kernels only (ru_on in
-// ntm_device.h), like D4 / D6: the reference's cost has none (Ru = 0).
+// ntm_device.h), like D4 / D6: the reference's cost has none (Ru = 0).  So is a
+// stage weight other than the reference's Q = I (NTM_MPC_Sim.m:59; qi_on): the
+// specialised kernels take the identity for Om.
+bool q_is_identity(const ntm_config* c) { return c->Q[0] == 1.0 && c->Q[1] == 0.0 && c->Q[2] == 0.0 && c->Q[3] == 1.0; }
 bool use_generic(const ntm_config* c) {
     return force_generic() || (c->flags & kGenericOnlyFlags) != 0 || (c->N == 20 && c->mode == NTM_MODE_FULL_DU) ||
-           c->Ru != 0.0;
+           c->Ru != 0.0 || !q_is_identity(c);
 }
 #ifdef NTM_RU_ONLY20
 // resource-usage check of the N=20 hot kernel alone (make ru20): every horizon
