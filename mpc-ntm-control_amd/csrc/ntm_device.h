@@ -187,7 +187,8 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        CN_FAIL_IT1, CN_FAIL_IT2, CN_GI_IT1, CN_GI_IT2, CN_GI_LATE, CN_TRY_IT1, CN_TRY_IT2, CN_WARM_TRY, CN_WARM_OK, CN_WARM_DEP, CN_WARM_NEG, CN_WARM_FULL, CN_ALT_TRY, CN_ALT_HIT,
        ST_K_Y, ST_K_CHK, ST_K_GRAD, ST_K_MU, ST_K_SUB, ST_C_A, ST_C_B, ST_C_Y, ST_C_SQ,
        ST_SC_COL, ST_SC_ROW, ST_SC_END, ST_L_COEF, ST_L_LOOP, CN_CYC_HIT, CN_CYC_SKIP,
-       CN_FK_DUAL, CN_FK_PRIMAL, CN_FK_SING, CN_FK_BOTH, ST_GI_WARM };
+       CN_FK_DUAL, CN_FK_PRIMAL, CN_FK_SING, CN_FK_BOTH, ST_GI_WARM,
+       CN_CDP_DROP, CN_CDP_RES, CN_CDP_PART, CN_CDP_DIR, CN_CDP_GI };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 #ifndef NTM_MAX_NT
 #define NTM_MAX_NT 32
@@ -196,7 +197,16 @@ constexpr int kMaxNT = NTM_MAX_NT; // explicit R^{-1} in GI up to this horizon (
 #ifndef NTM_REPAIRS
 #define NTM_REPAIRS 8
 #endif
-constexpr int kRepairs = NTM_REPAIRS;   // also at N = 50: 16 / 32 were no faster in mode 2, 6% / 10% slower in mode 3
+constexpr int kRepairs = NTM_REPAIRS;
+// NTM_CDP=1: a failed candidate continues on Goldfarb-Idnani's dual path with certified
+// re-solves (qp_phase); up to N + kCdpExtra re-solves before GI itself takes over
+#ifndef NTM_CDP
+#define NTM_CDP 1
+#endif
+#ifndef NTM_CDP_EXTRA
+#define NTM_CDP_EXTRA 8
+#endif
+constexpr int kCdpExtra = NTM_CDP_EXTRA;   // also at N = 50: 16 / 32 were no faster in mode 2, 6% / 10% slower in mode 3
 // A constant row (Lin_i = 0: the x_0 rows of getWLc, state rows Gamma doesn't
 // reach) is violated when b_i < -kConstTol (D22, oracle CONST_ROW_TOL): the same
 // absolute 1e-9 the KKT certificate allows on a unit-scale row.  An exact test
@@ -2314,12 +2324,21 @@ __device__ __forceinline__ bool polish_phase(const Prob& pb, const W& w, const R
 // slack on every row, multiplier signs).  Writes w.U()/w.V() on success or
 // when !verify_only (then GI's V is kept); returns success.
 // ---------------------------------------------------------------------------
+// mult_out (optional, LDS): every active row's multiplier (GI form, n'V >= bc rows),
+// by active position, written when the certificate's multipliers are formed.
+// dir_p >= 0 (the certified dual path of qp_phase): no solve at all.  The active
+// set of q rows must be echelon (sq); the certificate's multiplier pass then runs
+// with row dir_p's normal n_p in place of the gradient, i.e. it writes to mult_out
+// the r with sum_i r_i n_i = n_p (n_p dependent on the set: Goldfarb-Idnani's
+// dual-only step direction).  Returns false for any other set.  V and U are left
+// untouched.
 template <int P, class W>
 __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const StructRows rows, int q, int l, bool verify_only,
                                int* ns_out, int* fail_kind = nullptr, int* fail_pos = nullptr,
-                               double* v_out = nullptr) {
+                               double* v_out = nullptr, double* mult_out = nullptr, int dir_p = -1) {
     const int N = w.n(), LD = w.ldj(), LDJ = w.ldj();
     const OmQ<qi_on<W>()> om(pb.Q);
+    const bool dir = dir_p >= 0;
     const double Vprev = (l < N) ? w.V()[l] : 0.0;
     NTM_T0(tp);
     // --- classify active rows: single-entry rows fix a variable, the rest are general ---
@@ -2410,7 +2429,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     // all-LDS and generic builds; the far N = 20 / 50 kernels keep one code path)
     constexpr bool kFixedY = !W::kFar;
     const bool allfixed = kFixedY && nF == 0 && nS == 0;
-    for (int r = l; r < 2 * N; r += P) {
+    for (int r = l; r < 2 * N && !dir; r += P) {
         const double y = gamma_row_dot<NTM_CH>(w, r, w.dr());
         w.Phi()[r] = y;
         w.xp()[r] = allfixed ? y : y + w.e()[r] - ((r & 1) ? pb.r[1] : pb.r[0]);
@@ -2484,6 +2503,10 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         }
     }
     NTM_ACC(ST_C_SQ, tp);
+    if (dir && !sq) {                                      // the dual path's direction: echelon sets only
+        if (fail_kind) *fail_kind = 3;
+        return false;
+    }
     // --- g_F (lane a = compact index) ---
     double gl = 0.0;
     if (!sq && l < nF) {
@@ -2641,15 +2664,16 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         }
         }
         double acc = 0.0, acz = 0.0, acz2 = 0.0;
-        if (l < n) {
+        if (l < n && !dir) {
             acc = hs_of(perm[l]);
             if (nc >= 0 && nc < pc(l)) acz = -gen_n(perm[l], w.fidx()[nc]);
             if (kCollision && nc2 >= 0 && nc2 < pc(l)) acz2 = -gen_n(perm[l], w.fidx()[nc2]);
         }
-        const double hxb = (kCollision && xb >= 0) ? hs_of(xb) : 0.0;   // before w.Phi() is reused
+        const double hxb = (kCollision && xb >= 0 && !dir) ? hs_of(xb) : 0.0;   // before w.Phi() is reused
         NTM_WSYNC();
         if (l < n) sq_id = 1.0 / Ep[w.eidx(l, l)];
         NTM_ACC(ST_S_E, tp);
+        if (!dir) {
         // E_p V_p = h and (k = 1) E_p Z_p = -e_c: lane t owns row t; step t broadcasts
         // x_t (z_t) and updates the rows below
         double x = 0.0, zz = 0.0, zz2 = 0.0;
@@ -2748,6 +2772,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             for (int r = l; r < 2 * N; r += P) w.xp()[r] += wv * w.Phi()[r];   // y = y0 + w yz
             y_ready = true;
         }
+        }   // !dir
         if (!ok) fk = 3;
         NTM_ACC(ST_S_Y, tp);
     } else if (fused) {
@@ -3047,6 +3072,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     for (int pass = 0; ok; ++pass) {
         // ---- KKT certificate ----
         const bool resid = refine && pass == 0;
+        if (!dir) {
         if (l < N) { w.V()[l] = vfin; w.U()[l] = w.D()[l] * vfin; }
         NTM_WSYNC();
         // y = Gamma U once, for the primal check (state rows) and the gradient
@@ -3054,9 +3080,11 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             for (int r = l; r < 2 * N; r += P) w.xp()[r] = gamma_row_dot<NTM_CH>(w, r, w.U());
             NTM_WSYNC();
         }
+        }
         NTM_ACC(ST_K_Y, tp);
         Pick vf{};
-        if (resid) {
+        if (dir) {
+        } else if (resid) {
             if (l < nS) {                                  // primal residual of general row l
                 const int r = w.srw()[l];
                 const double sg = w.ssg()[l];
@@ -3080,19 +3108,23 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         // below uses its first nS entries, the refinement its first nt <= 2N): y
         // itself stays in w.xp(), where the rollout of a certified U reads it
         double* const omy = w.Phi() + 2 * N;
+        double res = 0.0;
+        if (dir) {                                         // n_p in place of the gradient
+            if (l < N) res = -((rows.lin(w, dir_p, l) * w.D()[l]) / rows.rnorm(w, dir_p));
+        } else {
         if (l < N) {
             const double y0 = w.xp()[2 * l], y1 = w.xp()[2 * l + 1];
             omy[2 * l] = om.o0(y0, y1);
             omy[2 * l + 1] = om.o1(y0, y1);
         }
         NTM_WSYNC();
-        double res = 0.0;
         if (l < N) {
             const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;
             const double g2 = dot_rows2<NTM_CH>(cl, omy, N, l);      // terms i < l masked
             double gu = 2 * g2;
             if constexpr (ru_on<W>()) gu = gu + 2 * pb.Ru * w.U()[l];  // + 2 Ru U_l
             res = w.D()[l] * gu + w.F()[l];
+        }
         }
         NTM_ACC(ST_K_GRAD, tp);
         if (sq) {
@@ -3247,6 +3279,15 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 continue;
             }
         }
+        if (mult_out) {                                    // by active position
+            if (l < nS) mult_out[w.sidx()[l]] = w.np()[l];
+            if (fixed) mult_out[w.fx()[l] - 1] = res / w.hv()[l];
+        }
+        if (dir) {
+            ok = gmaxi<P>(((l < nS && !isfinite(w.np()[l])) || (fixed && !isfinite(res / w.hv()[l]))) ? 1 : 0) == 0;
+            fk = ok ? 0 : 3;
+            break;
+        }
         // multipliers: general row s on lane s, fixed variable j on lane j; each
         // lane keeps its most negative one and that row's active-list position
         double mval = 0.0;
@@ -3274,6 +3315,10 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     if (fail_kind) *fail_kind = uni<P>(fk);
     if (fail_pos) *fail_pos = uni<P>(fpos_out);
     if (v_out) *v_out = vfin;
+    if (dir) {
+        NTM_WSYNC();
+        return ok;
+    }
     if (verify_only && !ok) {
         if (l < N) w.V()[l] = Vprev;
         NTM_WSYNC();
@@ -3551,6 +3596,173 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                 for (int i = 0; i < cq; ++i) NTM_TRACE(" %d", w.act()[i]);
                 NTM_TRACE("\n");
 #endif
+#if NTM_CDP
+                // Certified dual path (round 5).  The candidate's re-solve either
+                // certifies, or it gives the set's equality-constrained optimum and
+                // multipliers.  A set whose multipliers are not all >= 0 first drops
+                // its most negative one, re-solving each time, until it is dual
+                // feasible.  From there Goldfarb & Idnani's dual method runs with
+                // certified re-solves as its linear algebra: the most violated row p
+                // is added; the re-solve on A + {p} is the end point of GI's (linear)
+                // step, so a multiplier of A that is negative there is dropped at the
+                // fraction of the step where it reaches zero (V and the multipliers
+                // interpolated), and A - {i} + {p} is re-solved; a row p dependent on
+                // A (a full set: q = N) takes GI's dual-only step, with r from the
+                // certificate's multiplier pass on n_p (polish_compact, dir_p).  The
+                // last re-solve of a full step that passes the KKT certificate is
+                // the answer.  Offline (tools/repair_study.py, N = 20 mode 2, steps
+                // 6-25): every iteration-2 QP certifies, 3.2 re-solves on average,
+                // where the single-row repairs left 16% to Goldfarb-Idnani.  GI itself
+                // (warm from the current set) is the fallback when the budget runs
+                // out or the set degenerates.
+                // Iteration 2: a singular carried set is replaced by the other form
+                // (shifted or unshifted) of the previous step's last even set.
+                bool alt = it == 2 && pb.mode != NTM_MODE_NONE;
+                const int budget = N + kCdpExtra;
+                // drop position `pos` of the active list (and of the lane-per-position u)
+                auto drop_at = [&](int pos, double& u) {
+                    int an = 0;
+                    if (l >= pos && l + 1 < cq) an = w.act()[l + 1];
+                    const double un = __shfl(u, (l + 1) & (P - 1), P);
+                    NTM_WSYNC();
+                    if (l >= pos && l + 1 < cq) w.act()[l] = an;
+                    if (l >= pos) u = (l + 1 < cq) ? un : 0.0;
+                    --cq;
+                    NTM_WSYNC();
+                };
+                // One polish_compact call site (the kernel inlines it): each trip re-solves
+                // qs rows (A, or A + {p} at position cq) or, with dirp >= 0, takes the
+                // dual-only direction of row dirp on A.  stage 0: the carried set;
+                // 1: dropping negative multipliers; 2: A + {p}; 3: the direction of p
+                int stage = 0, qs = cq, dirp = -1, p = -1, nres = 0, fk = 0, fp = 0;
+                double vf = 0.0, V0 = 0.0, u0 = 0.0;   // V0: lane = variable; u0: lane = active position
+                bool okc = false;
+                for (;;) {
+                    if (n_try && dirp < 0) ++*n_try;
+                    const bool oks = polish_compact<P>(pb, w, rows, qs, l, true, &ns, &fk, &fp, &vf, w.uu(), dirp);
+                    NTM_TRACE("QP cdp stage %d qs %d dir %d ok %d fk %d fp %d\n", stage, qs, dirp, (int)oks, fk, fp);
+                    ++nres;
+                    bool pick = false;
+                    if (stage == 0) {
+                        if (it <= 2) NTM_CNT(CN_TRY_EARLY);
+                        if (!oks) { if (it <= 2) NTM_CNT(CN_FAIL_EARLY); else NTM_CNT(CN_FAIL_LATE); }
+                        if (it <= 2 && !oks) {
+                            if (fk == 1) NTM_CNT(CN_FK_DUAL);
+                            else if (fk == 2) NTM_CNT(CN_FK_PRIMAL);
+                            else if (fk == 3) NTM_CNT(CN_FK_SING);
+                            else NTM_CNT(CN_FK_BOTH);
+                        }
+                        if (it == 1) { NTM_CNT(CN_TRY_IT1); if (!oks) NTM_CNT(CN_FAIL_IT1); }
+                        if (it == 2) { NTM_CNT(CN_TRY_IT2); if (!oks) NTM_CNT(CN_FAIL_IT2); }
+                        if (oks) { okc = true; break; }
+                        if (fk == 3) {                     // singular: the other form of the carried set
+                            if (!alt) break;
+                            alt = false;
+                            NTM_CNT(CN_ALT_TRY);
+                            if (shift_first) {
+                                cq = cq0;
+                                if (l < cq) w.act()[l] = cand[l];
+                                NTM_WSYNC();
+                            } else {
+                                cq = shifted_into_act<P>(pb, w, cand, l);
+                            }
+                            qs = cq;
+                            continue;
+                        }
+                        stage = 1;
+                    }
+                    if (stage == 1) {                      // dual feasibility first
+                        if (oks) { okc = true; break; }
+                        if (fk == 1 || fk == 4) {
+                            if (nres >= budget) break;
+                            double ud = 0.0;
+                            drop_at(fp, ud);
+                            qs = cq;
+                            NTM_CNT(CN_CDP_DROP);
+                            continue;
+                        }
+                        if (fk != 2) break;
+                        V0 = vf;
+                        u0 = (l < cq) ? w.uu()[l] : 0.0;
+                        pick = true;
+                    } else if (stage == 2) {               // the end point of adding p
+                        NTM_CNT(CN_CDP_RES);
+                        if (oks) { ++cq; okc = true; break; }
+                        if (fk == 3) {                     // A + {p} singular: p depends on A
+                            dirp = p;
+                            qs = cq;
+                            stage = 3;
+                            continue;
+                        }
+                        const double u1 = (l <= cq) ? w.uu()[l] : 0.0;
+                        double th = (l < cq && u1 < 0.0) ? u0 / (u0 - u1) : kInf;
+                        int li = l;
+                        gargmin<P>(th, li);
+                        if (!(th < kInf)) {                // full step: p joins A
+                            ++cq;
+                            u0 = (l < cq) ? u1 : 0.0;
+                            V0 = vf;
+                            if (fk != 2) break;            // (a multiplier < 0 only by rounding: GI)
+                            pick = true;
+                        } else {                           // partial step: row li reaches u = 0 and leaves
+                            V0 += th * (vf - V0);
+                            u0 += th * (u1 - u0);
+                            drop_at(li, u0);
+                            NTM_CNT(CN_CDP_PART);
+                        }
+                    } else {                               // dual-only step: n_p = sum_i r_i n_i over A
+                        NTM_CNT(CN_CDP_DIR);
+                        dirp = -1;
+                        if (!oks) break;
+                        const double r = (l < cq) ? w.uu()[l] : 0.0;
+                        double tt = (l < cq && r > 0.0) ? u0 / r : kInf;
+                        int li = l;
+                        gargmin<P>(tt, li);
+                        if (!(tt < kInf)) break;           // no row can leave: GI decides (infeasible)
+                        u0 -= tt * r;
+                        drop_at(li, u0);
+                    }
+                    if (pick) {                            // the most violated row at V0 (y of the last re-solve in w.xp())
+                        if (l < cq) w.aflag()[w.act()[l]] = kActiveRow;
+                        NTM_WSYNC();
+                        const double vmx = fmax(1.0, gmax<P>(l < N ? fabs(V0) : 0.0));
+                        const Pick pk = rows.template check<P>(w, V0, l, false, vmx, w.xp());
+                        NTM_WSYNC();
+                        if (l < cq) w.aflag()[w.act()[l]] = 0;
+                        NTM_WSYNC();
+                        if (pk.p < 0 || !(pk.s < -1e-9 * fmax(vmx, fabs(pk.bc)))) break;
+                        p = pk.p;
+                    }
+                    if (nres >= budget) break;             // add p: A + {p}, or its direction when A is full
+                    if (cq >= N) {
+                        dirp = p;
+                        qs = cq;
+                        stage = 3;
+                    } else {
+                        if (l == 0) w.act()[cq] = p;
+                        NTM_WSYNC();
+                        qs = cq + 1;
+                        stage = 2;
+                    }
+                }
+                if (okc) {
+                    flag = NTM_EXIT_OPTIMAL;
+                    q = cq;
+                    done = true;
+                    yv = true;
+                    NTM_CNT(CN_HIT);
+                    if (nres > 1) NTM_CNT(CN_REPAIR);
+                } else {
+                    NTM_CNT(CN_CDP_GI);
+                    // GI warm from the current set (dual feasible on the primal phase)
+                    if (l < cq) {
+                        w.aflag()[w.act()[l]] = kCandRow;
+                        w.sidx()[l] = w.act()[l];
+                    }
+                    nwarm = cq;
+                    NTM_WSYNC();
+                }
+#else
                 // iteration 2: the carried set is the previous step's (slot 1 is only
                 // written at even iterations); when its repairs fail, its
                 // receding-horizon shift is tried before GI (it hits in the
@@ -3688,6 +3900,7 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                     nwarm = cq;
                     NTM_WSYNC();
                 }
+#endif
                 NTM_ACC(ST_CAND, tq);
             }
             if (!done) {

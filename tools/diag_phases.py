@@ -57,5 +57,7 @@ for i, n in enumerate(fine):
     print(f"  {n:9s} {buf[46 + i]/B:12.0f}")
 print(f"exact 2-cycle study: steps whose rho and U after iteration it equal those after it-2 (it >= 3): "
       f"{buf[60]/B:.4f} per wave-step; iterations a shortcut could skip {buf[61]/B:.4f} per wave-step")
+print(f"certified dual path per wave-step: negative-multiplier drops {buf[67]/B:.3f}, A+p re-solves {buf[68]/B:.3f}, "
+      f"partial steps {buf[69]/B:.3f}, dual-only directions {buf[70]/B:.3f}, handed to GI {buf[71]/B:.3f}")
 print(f"first tries at it<=2 that failed, by kind, per wave-step: dual {buf[62]/B:.3f}, primal {buf[63]/B:.3f}, "
       f"singular/colliding {buf[64]/B:.3f}, primal and dual {buf[65]/B:.3f}")
