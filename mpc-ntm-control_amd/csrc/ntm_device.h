@@ -188,7 +188,8 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        ST_K_Y, ST_K_CHK, ST_K_GRAD, ST_K_MU, ST_K_SUB, ST_C_A, ST_C_B, ST_C_Y, ST_C_SQ,
        ST_SC_COL, ST_SC_ROW, ST_SC_END, ST_L_COEF, ST_L_LOOP, CN_CYC_HIT, CN_CYC_SKIP,
        CN_FK_DUAL, CN_FK_PRIMAL, CN_FK_SING, CN_FK_BOTH, ST_GI_WARM,
-       CN_CDP_DROP, CN_CDP_RES, CN_CDP_PART, CN_CDP_DIR, CN_CDP_GI };
+       CN_CDP_DROP, CN_CDP_RES, CN_CDP_PART, CN_CDP_DIR, CN_CDP_GI,
+       CN_CDPX_SING0, CN_CDPX_SING1, CN_CDPX_BUDGET, CN_CDPX_DIR, CN_CDPX_NOVIOL, CN_CDPX_FULLDUAL, CN_CDPX_TINF };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 #ifndef NTM_MAX_NT
 #define NTM_MAX_NT 32
@@ -3656,7 +3657,7 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                         if (it == 2) { NTM_CNT(CN_TRY_IT2); if (!oks) NTM_CNT(CN_FAIL_IT2); }
                         if (oks) { okc = true; break; }
                         if (fk == 3) {                     // singular: the other form of the carried set
-                            if (!alt) break;
+                            if (!alt) { NTM_CNT(CN_CDPX_SING0); break; }
                             alt = false;
                             NTM_CNT(CN_ALT_TRY);
                             if (shift_first) {
@@ -3674,14 +3675,14 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                     if (stage == 1) {                      // dual feasibility first
                         if (oks) { okc = true; break; }
                         if (fk == 1 || fk == 4) {
-                            if (nres >= budget) break;
+                            if (nres >= budget) { NTM_CNT(CN_CDPX_BUDGET); break; }
                             double ud = 0.0;
                             drop_at(fp, ud);
                             qs = cq;
                             NTM_CNT(CN_CDP_DROP);
                             continue;
                         }
-                        if (fk != 2) break;
+                        if (fk != 2) { NTM_CNT(CN_CDPX_SING1); break; }
                         V0 = vf;
                         u0 = (l < cq) ? w.uu()[l] : 0.0;
                         pick = true;
@@ -3702,7 +3703,10 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                             ++cq;
                             u0 = (l < cq) ? u1 : 0.0;
                             V0 = vf;
-                            if (fk != 2) break;            // (a multiplier < 0 only by rounding: GI)
+                            // a negative multiplier at the end point now (p's own: an ill-conditioned
+                            // step at long horizons) goes to GI; dropping it and continuing measured
+                            // slower (config 5 mode 2: 112 -> 156 ms per step-batch, A/B on one box)
+                            if (fk != 2) { NTM_CNT(CN_CDPX_FULLDUAL); break; }
                             pick = true;
                         } else {                           // partial step: row li reaches u = 0 and leaves
                             V0 += th * (vf - V0);
@@ -3713,12 +3717,12 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                     } else {                               // dual-only step: n_p = sum_i r_i n_i over A
                         NTM_CNT(CN_CDP_DIR);
                         dirp = -1;
-                        if (!oks) break;
+                        if (!oks) { NTM_CNT(CN_CDPX_DIR); break; }
                         const double r = (l < cq) ? w.uu()[l] : 0.0;
                         double tt = (l < cq && r > 0.0) ? u0 / r : kInf;
                         int li = l;
                         gargmin<P>(tt, li);
-                        if (!(tt < kInf)) break;           // no row can leave: GI decides (infeasible)
+                        if (!(tt < kInf)) { NTM_CNT(CN_CDPX_TINF); break; }   // no row can leave: GI decides (infeasible)
                         u0 -= tt * r;
                         drop_at(li, u0);
                     }
@@ -3730,10 +3734,10 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                         NTM_WSYNC();
                         if (l < cq) w.aflag()[w.act()[l]] = 0;
                         NTM_WSYNC();
-                        if (pk.p < 0 || !(pk.s < -1e-9 * fmax(vmx, fabs(pk.bc)))) break;
+                        if (pk.p < 0 || !(pk.s < -1e-9 * fmax(vmx, fabs(pk.bc)))) { NTM_CNT(CN_CDPX_NOVIOL); break; }
                         p = pk.p;
                     }
-                    if (nres >= budget) break;             // add p: A + {p}, or its direction when A is full
+                    if (nres >= budget) { NTM_CNT(CN_CDPX_BUDGET); break; }   // add p: A + {p}, or its direction when A is full
                     if (cq >= N) {
                         dirp = p;
                         qs = cq;

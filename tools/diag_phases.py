@@ -59,5 +59,8 @@ print(f"exact 2-cycle study: steps whose rho and U after iteration it equal thos
       f"{buf[60]/B:.4f} per wave-step; iterations a shortcut could skip {buf[61]/B:.4f} per wave-step")
 print(f"certified dual path per wave-step: negative-multiplier drops {buf[67]/B:.3f}, A+p re-solves {buf[68]/B:.3f}, "
       f"partial steps {buf[69]/B:.3f}, dual-only directions {buf[70]/B:.3f}, handed to GI {buf[71]/B:.3f}")
+print(f"  handed to GI because: candidate singular {buf[72]/B:.3f}, singular in the dual phase {buf[73]/B:.3f}, budget {buf[74]/B:.3f}, "
+      f"direction on a non-echelon set {buf[75]/B:.3f}, no violated row {buf[76]/B:.3f}, dual failure at a full step {buf[77]/B:.3f}, "
+      f"no row can leave {buf[78]/B:.3f}")
 print(f"first tries at it<=2 that failed, by kind, per wave-step: dual {buf[62]/B:.3f}, primal {buf[63]/B:.3f}, "
       f"singular/colliding {buf[64]/B:.3f}, primal and dual {buf[65]/B:.3f}")

@@ -108,8 +108,8 @@ class QP:
         return fk, U, mu, s
 
 
-def device_repair(qp, cand, alt_set, budget=8, multi_drop=False):
-    """qp_phase's loop: returns (certified, re-solves)."""
+def device_repair(qp, cand, alt_set, budget=8, multi_drop=False, out=None):
+    """qp_phase's loop: returns (certified, re-solves); out[0]: the last set."""
     act, n = list(cand), 0
     alt = alt_set is not None
     rep = 0
@@ -141,11 +141,23 @@ def device_repair(qp, cand, alt_set, budget=8, multi_drop=False):
             act = [a for k2, a in enumerate(act) if k2 != fp]
         if stop:
             if not alt:
+                if out is not None:
+                    out.append(act)
                 return False, n
             alt = False
             act = list(alt_set)
             rep = -2
         rep += 1
+
+
+def hybrid(qp, cand, alt_set, reps, budget=64):
+    """reps single-row repairs, then the certified dual path from the set they reach."""
+    out = []
+    ok, n = device_repair(qp, cand, None, reps, out=out)
+    if ok:
+        return True, n
+    ok2, n2 = gi_resolve(qp, out[0] if out else cand, None, budget)
+    return ok2, n + n2
 
 
 def device_revert(qp, cand, alt_set, budget=8, max_skip=99):
@@ -320,6 +332,9 @@ strategies = {
     "device (16 repairs)": lambda q, c, a: device_repair(q, c, a, 16),
     "GI by re-solves (16)": lambda q, c, a: gi_resolve(q, c, a, 16),
     "GI by re-solves (64)": lambda q, c, a: gi_resolve(q, c, a, 64),
+    "1 repair + GI by re-solves": lambda q, c, a: hybrid(q, c, a, 1),
+    "2 repairs + GI by re-solves": lambda q, c, a: hybrid(q, c, a, 2),
+    "4 repairs + GI by re-solves": lambda q, c, a: hybrid(q, c, a, 4),
 }
 res = {it: {k: [0, 0, 0] for k in strategies} for it in ITERS}   # certified, re-solves, count
 exact = {it: 0 for it in ITERS}
