@@ -441,12 +441,26 @@ __device__ __forceinline__ double coef_b(const Coef& k, double r3) { return k.bc
 #define NTM_FAR_COLMAJOR 0   // 1: J, T and the bordered factor column-major in the far block (slower)
 #endif
 __host__ __device__ constexpr bool ws_far(int NN) { return NN > 32 || (NTM_FAR_N20 && NN == 20); }
+// The slim far layout (N = 20 far, round 5): 16 scenarios per CU (4 waves per SIMD,
+// <= 10,240 B of LDS each) instead of 12.  What leaves LDS: the A/B coefficient
+// arrays (each lane keeps its stage's in registers, broadcast by readlane in the
+// lift), Phi and Lambda (the lift runs the free response e = Phi x_k + Lambda as a
+// recursion of its own, one more lane; 2N of the old Phi stay as the re-solve's
+// scratch), the hoisted V-space box (vlo / vhi, recomputed from D), and the
+// diagonal reciprocals of the bordered factor and GI's Cholesky (ldi / kdi), which
+// move to the far block with the rate-row norms (idun, mode 3 never runs here).
+// The Om products are the identity (qi_on), so the certificate's Om y is y itself.
+#ifndef NTM_SLIM20
+#define NTM_SLIM20 1
+#endif
+__host__ __device__ constexpr bool ws_slim(int N, bool far) { return NTM_SLIM20 && far && N == 20; }
 
 template <int NN, bool GEN = false, bool FAR = ws_far(NN)>
 struct WS {
     static constexpr int kNN = NN;
     static constexpr bool kGen = GEN;
     static constexpr bool kFar = FAR;
+    static constexpr bool kSlim = ws_slim(NN, FAR);
     int N_rt;
     double* base;
     double* far;       // kFar: this scenario's J/R block in HBM
@@ -454,7 +468,7 @@ struct WS {
     __device__ __forceinline__ int ldj() const { return n() | 1; }
     __device__ __forceinline__ int ldg() const { return 2 * n(); }
     // double offsets of each array (n() is launch-uniform, so these fold to scalar math)
-    __device__ __forceinline__ int oJ() const { return 14 * n() + n() * (n() + 1); }
+    __device__ __forceinline__ int oJ() const { return (kSlim ? 7 : 14) * n() + n() * (n() + 1); }
     __device__ __forceinline__ int oR() const { return oJ() + n() * ldj(); }
     // T = R^{-1} is kept for N <= kMaxNT only: at long horizons its N^2 doubles would
     // halve the scenarios per CU, and the dual direction falls back to back substitution.
@@ -469,14 +483,15 @@ struct WS {
         else return oT() + (useT() ? n() * ldj() : 0);   // vector block
     }
     __device__ __forceinline__ double* rho() const { return base; }                 // 3N (3xN col-major)
+    // (kSlim: no a11 / a21 / bb / Lam, Phi is 2N of scratch; never called there)
     __device__ __forceinline__ double* a11() const { return base + 3 * n(); }         // n()
     __device__ __forceinline__ double* a21() const { return base + 4 * n(); }         // n()
     __device__ __forceinline__ double* bb() const { return base + 5 * n(); }          // n()
-    __device__ __forceinline__ double* Phi() const { return base + 6 * n(); }         // 4N Phi_i (2x2 col-major)
+    __device__ __forceinline__ double* Phi() const { return base + (kSlim ? 3 : 6) * n(); }   // 4N Phi_i (2x2 col-major)
     __device__ __forceinline__ double* Lam() const { return base + 10 * n(); }        // 2N
-    __device__ __forceinline__ double* e() const { return base + 12 * n(); }          // 2N free response
+    __device__ __forceinline__ double* e() const { return base + (kSlim ? 5 : 12) * n(); }    // 2N free response
     // Gamma, block-lower-triangular and packed by column: column j holds rows 2j..2N-1
-    __device__ __forceinline__ double* Gt() const { return base + 14 * n(); }         // n()(n()+1)
+    __device__ __forceinline__ double* Gt() const { return base + (kSlim ? 7 : 14) * n(); }   // n()(n()+1)
     __device__ __forceinline__ int gidx(int r, int j) const { return j * (2 * n() - j + 1) + r - 2 * j; }
     __device__ __forceinline__ double& gt(int r, int j) const { return Gt()[gidx(r, j)]; }   // r >= 2j
     __device__ __forceinline__ double* J() const {                                   // n() x ldj() row-major
@@ -561,30 +576,40 @@ struct WS {
     // 2N ints (in 2N doubles of space): per state row r, (last column j with
     // Gamma_rj != 0) + 1, plus kRowMulti if it has two or more non-zeros
     __device__ __forceinline__ int* rinfo() const { return reinterpret_cast<int*>(base + oV()); }
-    __device__ __forceinline__ double* F() const { return base + oV() + 2 * n(); }    // n()  F~
-    __device__ __forceinline__ double* D() const { return base + oV() + 3 * n(); }    // n()  Jacobi scaling
-    __device__ __forceinline__ double* V() const { return base + oV() + 4 * n(); }    // n()  scaled variables
-    __device__ __forceinline__ double* d() const { return base + oV() + 5 * n(); }    // n()
-    __device__ __forceinline__ double* np() const { return base + oV() + 6 * n(); }   // n()  GI normal
-    __device__ __forceinline__ double* hv() const { return base + oV() + 7 * n(); }   // n()  Householder / polish
-    __device__ __forceinline__ double* Vb() const { return base + oV() + 8 * n(); }   // n()  polish fixed (V)
-    __device__ __forceinline__ double* Uf() const { return base + oV() + 9 * n(); }   // n()  polish fixed (U)
-    __device__ __forceinline__ double* uu() const { return base + oV() + 10 * n(); }  // n()+1 multipliers
-    __device__ __forceinline__ double* xp() const { return base + oV() + 11 * n() + 1; }   // 2(n()+1) rollout
-    __device__ __forceinline__ double* U() const { return base + oV() + 13 * n() + 3; }    // n()
-    __device__ __forceinline__ double* Uold() const { return base + oV() + 14 * n() + 3; } // n()
-    __device__ __forceinline__ double* dr() const { return base + oV() + 15 * n() + 3; }    // N: d masked to b < q (GI)
-    // per-QP constants hoisted out of the solver loops
-    __device__ __forceinline__ double* vlo() const { return base + oV() + 16 * n() + 3; }   // N: umin/D_j
-    __device__ __forceinline__ double* vhi() const { return base + oV() + 17 * n() + 3; }   // N: umax/D_j
-    __device__ __forceinline__ double* irn() const { return base + oV() + 18 * n() + 3; }   // 2N: 1/rn_r (0: const row)
-    __device__ __forceinline__ double* ldi() const { return base + oV() + 20 * n() + 3; }   // N: 1/L(k,k) (Cholesky)
-    __device__ __forceinline__ double* kdi() const { return base + oV() + 21 * n() + 3; }   // N: 1/K(k,k) (Schur)
-    __device__ __forceinline__ double* ssg() const { return base + oV() + 22 * n() + 3; }   // N: sign of general row s
-    __device__ __forceinline__ double* idun() const { return base + oV() + 23 * n() + 3; }  // N: 1/|D (e_i - e_{i-1})|
+    // kSlim: the 2N rinfo ints take N doubles, and vlo / vhi / ldi / kdi / idun leave LDS
+    static constexpr int kRi = kSlim ? 1 : 2;                // doubles of rinfo per N
+    __device__ __forceinline__ double* F() const { return base + oV() + kRi * n(); }         // n()  F~
+    __device__ __forceinline__ double* D() const { return base + oV() + (kRi + 1) * n(); }   // n()  Jacobi scaling
+    __device__ __forceinline__ double* V() const { return base + oV() + (kRi + 2) * n(); }   // n()  scaled variables
+    __device__ __forceinline__ double* d() const { return base + oV() + (kRi + 3) * n(); }   // n()
+    __device__ __forceinline__ double* np() const { return base + oV() + (kRi + 4) * n(); }  // n()  GI normal
+    __device__ __forceinline__ double* hv() const { return base + oV() + (kRi + 5) * n(); }  // n()  Householder / polish
+    __device__ __forceinline__ double* Vb() const { return base + oV() + (kRi + 6) * n(); }  // n()  polish fixed (V)
+    __device__ __forceinline__ double* Uf() const { return base + oV() + (kRi + 7) * n(); }  // n()  polish fixed (U)
+    __device__ __forceinline__ double* uu() const { return base + oV() + (kRi + 8) * n(); }  // n()+1 multipliers
+    __device__ __forceinline__ double* xp() const { return base + oV() + (kRi + 9) * n() + 1; }    // 2(n()+1) rollout
+    __device__ __forceinline__ double* U() const { return base + oV() + (kRi + 11) * n() + 3; }    // n()
+    __device__ __forceinline__ double* Uold() const { return base + oV() + (kRi + 12) * n() + 3; } // n()
+    __device__ __forceinline__ double* dr() const { return base + oV() + (kRi + 13) * n() + 3; }    // N: d masked to b < q (GI)
+    __device__ __forceinline__ double* irn() const { return base + oV() + (kRi + 14) * n() + 3; }   // 2N: 1/rn_r (0: const row)
+    __device__ __forceinline__ double* ssg() const { return base + oV() + (kRi + 16) * n() + 3; }   // N: sign of general row s
+    // per-QP constants hoisted out of the solver loops (not kSlim: recomputed from D)
+    __device__ __forceinline__ double* vlo() const { return base + oV() + (kRi + 17) * n() + 3; }   // N: umin/D_j
+    __device__ __forceinline__ double* vhi() const { return base + oV() + (kRi + 18) * n() + 3; }   // N: umax/D_j
+    // 1/L(k,k) (Cholesky), 1/K(k,k) (Schur), contiguous; 1/|D (e_i - e_{i-1})|: in the far block when kSlim
+    __device__ __forceinline__ double* ldi() const {
+        if constexpr (kSlim) return far + n() * ldj() + (n() + 1) * ldj();
+        else return base + oV() + (kRi + 19) * n() + 3;
+    }
+    __device__ __forceinline__ double* kdi() const { return ldi() + n(); }
+    __device__ __forceinline__ double* idun() const {
+        if constexpr (kSlim) return ldi() + 2 * n();
+        else return base + oV() + (kRi + 21) * n() + 3;
+    }
+    static constexpr int kVec = kSlim ? 18 : 24;             // N-vectors of the block (+ 3 + 3 scn)
     // this scenario's C1, B.m gain and w_dep (scenario generator; read only when pb.g.phys_on)
-    __device__ __forceinline__ double* scn() const { return base + oV() + 24 * n() + 3; }
-    __device__ __forceinline__ int* act() const { return reinterpret_cast<int*>(base + oV() + 24 * n() + 6); }
+    __device__ __forceinline__ double* scn() const { return base + oV() + kVec * n() + 3; }
+    __device__ __forceinline__ int* act() const { return reinterpret_cast<int*>(base + oV() + kVec * n() + 6); }
     __device__ __forceinline__ int* sidx() const { return act() + n() + 1; }
     __device__ __forceinline__ int* cand() const { return act() + 2 * (n() + 1); }   // 2(n()+1): last two active sets
     __device__ __forceinline__ int* fidx() const { return act() + 4 * (n() + 1); }   // n()+1: free variables (polish)
@@ -597,11 +622,13 @@ struct WS {
 
 __host__ __device__ constexpr int ldj_of(int N) { return N | 1; }
 // the J/R block of a far layout, in HBM per scenario (no T: WS::useT)
-__host__ __device__ constexpr int far_doubles(int N) { return N * ldj_of(N) + (N + 1) * ldj_of(N); }
+__host__ __device__ constexpr int far_doubles(int N) {
+    return N * ldj_of(N) + (N + 1) * ldj_of(N) + (ws_slim(N, true) ? 3 * N : 0);   // + ldi, kdi, idun (slim)
+}
 __host__ __device__ constexpr int ws_doubles(int N, bool far = false) {
     // LDS: the E block (far), or J, R and (N <= kMaxNT) T
     const int jr = far ? (N * (N + 1)) / 2 + (N + 1) : (N <= kMaxNT ? 2 : 1) * N * ldj_of(N) + (N + 1) * ldj_of(N);
-    return 14 * N + N * (N + 1) + jr + 24 * N + 6;
+    return ws_slim(N, far) ? 7 * N + N * (N + 1) + jr + 18 * N + 6 : 14 * N + N * (N + 1) + jr + 24 * N + 6;
 }
 // workspace bytes with room for `rows` active-row flags: the structured rows of
 // the MPC step are at most 8N+2 (getWLc 6N+4 plus 2(N-1) rate rows); a dense
@@ -921,9 +948,61 @@ __device__ __forceinline__ void lift_literal(const Prob& pb, const W& w, const C
 }
 
 template <int P, class W>
-__device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l) {
+__device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l, double x0 = 0.0, double x1 = 0.0) {
     const int N = w.n();
     const Coef k = scn_coef(pb, w);
+    if constexpr (W::kSlim) {
+        // lane l < N keeps stage l's A/B coefficients in registers; the loop takes
+        // stage i's by readlane.  Lanes < N: Gamma columns (as below); lane N: the
+        // free response e = Phi x_k + Lambda as its own recursion e_i = A_i e_{i-1} + C
+        // with e_{-1} = x_k (CANON D4: Phi_i = A_i Phi_{i-1}; the same states as
+        // Phi x_k + Lambda to rounding), written straight to w.e()
+        double ra = 0.0, rc = 0.0, rbb = 0.0;
+        if (l < N) {
+            ra = coef_a11(k, w.rho()[3 * l]);
+            rc = coef_a21(k, w.rho()[3 * l + 1]);
+            rbb = coef_b(k, w.rho()[3 * l + 2]);
+        }
+        const double a0 = gbcast<P>(ra, 0), c0v = gbcast<P>(rc, 0);
+        NTM_T0(tlf);
+        if (l <= N) {
+            const bool gam = l < N;
+            double g0 = gam ? rbb : (a0 * x0 + k.C1);
+            double g1 = gam ? 0.0 : ((c0v * x0 + k.a22 * x1) + k.C2);
+            const double c0 = gam ? 0.0 : k.C1, c1 = gam ? 0.0 : k.C2;
+            double* const rec = gam ? w.Gt() + w.gidx(2 * l, l) - 2 * l : w.e();
+            rec[2 * (gam ? l : 0)] = g0;
+            rec[2 * (gam ? l : 0) + 1] = g1;
+            constexpr int CH = NTM_CH;
+            NTM_CHUNK_PRAGMA
+            for (int i0 = 1; i0 < N; i0 += CH) {
+                double ca[CH], cb[CH];
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    const int i = i0 + u;
+                    ca[u] = i < N ? gbcast<P>(ra, i) : 0.0;
+                    cb[u] = i < N ? gbcast<P>(rc, i) : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    const int i = i0 + u;
+                    if (i < N) {
+                        const double n0 = ca[u] * g0 + c0;
+                        const double n1 = (cb[u] * g0 + k.a22 * g1) + c1;
+                        const bool live = !gam || i > l;
+                        g0 = live ? n0 : g0;
+                        g1 = live ? n1 : g1;
+                        const int at = live ? i : l;
+                        rec[2 * at] = g0;
+                        rec[2 * at + 1] = g1;
+                    }
+                }
+            }
+        }
+        NTM_ACC(ST_L_LOOP, tlf);
+        NTM_WSYNC();
+        return;
+    } else {
     if (l < N) {
         w.a11()[l] = coef_a11(k, w.rho()[3 * l]);
         w.a21()[l] = coef_a21(k, w.rho()[3 * l + 1]);
@@ -1010,6 +1089,7 @@ __device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l) {
         }
     }
     NTM_WSYNC();
+    }
 }
 
 // free response e = Phi x_k + Lambda (the x-dependent part of NTM_MPC_Sim.m:121
@@ -1017,11 +1097,17 @@ __device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l) {
 template <int P, class W>
 __device__ __forceinline__ void free_response(const W& w, double x0, double x1, int l, const Prob* pw = nullptr) {
     for (int i = l; i < w.n(); i += P) {
-        const double* Ph = w.Phi() + 4 * i;
-        const double e0 = (Ph[0] * x0 + Ph[2] * x1) + w.Lam()[2 * i];
-        const double e1 = (Ph[1] * x0 + Ph[3] * x1) + w.Lam()[2 * i + 1];
-        w.e()[2 * i] = e0;
-        w.e()[2 * i + 1] = e1;
+        double e0, e1;
+        if constexpr (W::kSlim) {                // the lift wrote e itself
+            e0 = w.e()[2 * i];
+            e1 = w.e()[2 * i + 1];
+        } else {
+            const double* Ph = w.Phi() + 4 * i;
+            e0 = (Ph[0] * x0 + Ph[2] * x1) + w.Lam()[2 * i];
+            e1 = (Ph[1] * x0 + Ph[3] * x1) + w.Lam()[2 * i + 1];
+            w.e()[2 * i] = e0;
+            w.e()[2 * i + 1] = e1;
+        }
         if (pw) {
             // Om (e_i - r) per stage for the scaling pass's F (scratch in w.xp(): the
             // rollout consumed it and rewrites it; the re-solve recomputes it)
@@ -1269,8 +1355,10 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
         bad |= !isfinite(f) || !isfinite(Dl);
         w.F()[l] = f;
         // V-space box of u_l (bc of the two u rows; same expressions as the oracle's b/rn)
-        w.vlo()[l] = -((-pb.umin) / Dl);
-        w.vhi()[l] = pb.umax / Dl;
+        if constexpr (!W::kSlim) {
+            w.vlo()[l] = -((-pb.umin) / Dl);
+            w.vhi()[l] = pb.umax / Dl;
+        }
     }
     NTM_WSYNC();
     NTM_ACC(ST_SC_COL, tsc);
@@ -1502,8 +1590,15 @@ struct StructRows {
             if (key < bv || (key == bv && id < bid)) { bv = key; bid = id; bs = s; bbc = bcv; }
         };
         if (l < N) {
-            double lo = w.vlo()[l];
-            double hi = w.vhi()[l];
+            double lo, hi;
+            if constexpr (W::kSlim) {                         // (diag_scale_phase's expressions)
+                const double Dl = w.D()[l];
+                lo = -((-umin) / Dl);
+                hi = umax / Dl;
+            } else {
+                lo = w.vlo()[l];
+                hi = w.vhi()[l];
+            }
             int idl = (mode == NTM_MODE_BOX) ? l : 6 * l;
             int idh = (mode == NTM_MODE_BOX) ? N + l : 6 * l + 1;
             consider(Vl - lo, idl, lo);
@@ -3108,12 +3203,14 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         // scratch (w.Phi() + 2N: Phi is dead until the next lift; the sparse pass
         // below uses its first nS entries, the refinement its first nt <= 2N): y
         // itself stays in w.xp(), where the rollout of a certified U reads it
-        double* const omy = w.Phi() + 2 * N;
+        // (kSlim: Om = I, so Om y is y itself, read from w.xp())
+        static_assert(!W::kSlim || qi_on<W>(), "the slim layout needs Q = I (qi_on)");
+        double* const omy = W::kSlim ? w.xp() : w.Phi() + 2 * N;
         double res = 0.0;
         if (dir) {                                         // n_p in place of the gradient
             if (l < N) res = -((rows.lin(w, dir_p, l) * w.D()[l]) / rows.rnorm(w, dir_p));
         } else {
-        if (l < N) {
+        if (l < N && !W::kSlim) {
             const double y0 = w.xp()[2 * l], y1 = w.xp()[2 * l + 1];
             omy[2 * l] = om.o0(y0, y1);
             omy[2 * l + 1] = om.o1(y0, y1);
@@ -3382,9 +3479,15 @@ __device__ __forceinline__ bool rollout_phase(const Prob& pb, const W& w, double
 #pragma unroll
             for (int u = 0; u < CH; ++u) {
                 const int i = i0 + u;
-                ca[u] = i < N ? w.a11()[i] : 0.0;
-                cb[u] = i < N ? w.bb()[i] : 0.0;
-                cc[u] = i < N ? w.a21()[i] : 0.0;
+                if constexpr (W::kSlim) {           // the lift's coefficients, from this iteration's rho
+                    ca[u] = i < N ? coef_a11(k, w.rho()[3 * i]) : 0.0;
+                    cb[u] = i < N ? coef_b(k, w.rho()[3 * i + 2]) : 0.0;
+                    cc[u] = i < N ? coef_a21(k, w.rho()[3 * i + 1]) : 0.0;
+                } else {
+                    ca[u] = i < N ? w.a11()[i] : 0.0;
+                    cb[u] = i < N ? w.bb()[i] : 0.0;
+                    cc[u] = i < N ? w.a21()[i] : 0.0;
+                }
                 cu[u] = i < N ? w.U()[i] : 0.0;
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -3548,7 +3651,7 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
     const int N = w.n();
     bool yv = false;                                     // w.xp() holds Gamma U of the final U
     NTM_T0(tq);
-    lift_phase<P>(pb, w, l);
+    lift_phase<P>(pb, w, l, x0, x1);
     NTM_ACC(ST_LIFT, tq);
     free_response<P>(w, x0, x1, l, &pb);     // F is formed with the Jacobi scaling below
     NTM_ACC(ST_COST, tq);

@@ -145,7 +145,7 @@ __device__ __forceinline__ int mpc_step_dev(const Prob& pb, const W& w, double x
 #define NTM_HOT_WAVES_PER_EU 2
 #endif
 #ifndef NTM_N20_WAVES_PER_EU
-#define NTM_N20_WAVES_PER_EU (NTM_FAR_N20 ? 3 : 2)
+#define NTM_N20_WAVES_PER_EU (NTM_FAR_N20 ? (NTM_SLIM20 ? 4 : 3) : 2)
 #endif
 // Long horizons (NN > 32): the LDS workspace already limits a CU to fewer waves
 // than SIMDs, so the register budget of one wave per SIMD costs no occupancy and
