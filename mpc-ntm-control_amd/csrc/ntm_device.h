@@ -1809,7 +1809,7 @@ __device__ __forceinline__ double bwd_lanes(const double* L, const double* rdiag
 template <int P, class Rows, class W>
 __device__ __forceinline__ int gi_solve(const W& w, const Rows rows, bool has_rows, int nrows, int l, int* iters_out, int* q_out,
                         int nwarm = 0) {
-    const int N = w.n(), LD = w.ldj();
+    const int N = w.n();
     const int JR = w.jr(), JC = w.jc();     // J(r, c) at r JR + c JC (T alike)
     *iters_out = 0;
     *q_out = 0;

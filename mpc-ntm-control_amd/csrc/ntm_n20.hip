@@ -7,6 +7,9 @@
 // The chunk loops are unrolled twice, not fully: at 168 VGPRs full unrolling
 // spills 68 VGPRs (276 B of scratch per lane), unroll 2 spills 28 (132 B):
 //   CH = 5, full unroll: 10.83   unroll 1: 10.61   unroll 2: 10.38 ms
+// Round 5, the slim layout at 4 waves per SIMD (128 VGPRs), default scheduler:
+//   CH = 5, unroll 2: 6.68   unroll 1: 6.78   unroll 3: 10.08   CH = 6: 9.33
+//   CH = 4: 10.86   CH = 3: 10.07 ms (the last two with the max-memory-clause scheduler)
 #ifndef NTM_N20_CH
 #define NTM_N20_CH 5
 #endif
