@@ -454,6 +454,12 @@ __host__ __device__ constexpr bool ws_far(int NN) { return NN > 32 || (NTM_FAR_N
 #define NTM_SLIM20 1
 #endif
 __host__ __device__ constexpr bool ws_slim(int N, bool far) { return NTM_SLIM20 && far && N == 20; }
+// NTM_SLIM_AB: the slim layout keeps a11 / a21 in LDS after all (2N doubles, paid for by
+// active-row flags for the 6N+4 getWLc rows only: mode 3 never runs on these kernels)
+#ifndef NTM_SLIM_AB
+#define NTM_SLIM_AB 1
+#endif
+__host__ __device__ constexpr int slim_ab(int N, bool far) { return ws_slim(N, far) && NTM_SLIM_AB ? 2 : 0; }
 
 template <int NN, bool GEN = false, bool FAR = ws_far(NN)>
 struct WS {
@@ -468,7 +474,8 @@ struct WS {
     __device__ __forceinline__ int ldj() const { return n() | 1; }
     __device__ __forceinline__ int ldg() const { return 2 * n(); }
     // double offsets of each array (n() is launch-uniform, so these fold to scalar math)
-    __device__ __forceinline__ int oJ() const { return (kSlim ? 7 : 14) * n() + n() * (n() + 1); }
+    static constexpr int kAB = slim_ab(NN, FAR);           // kSlim: a11 / a21 (N each) in LDS
+    __device__ __forceinline__ int oJ() const { return (kSlim ? 7 + kAB : 14) * n() + n() * (n() + 1); }
     __device__ __forceinline__ int oR() const { return oJ() + n() * ldj(); }
     // T = R^{-1} is kept for N <= kMaxNT only: at long horizons its N^2 doubles would
     // halve the scenarios per CU, and the dual direction falls back to back substitution.
@@ -487,11 +494,11 @@ struct WS {
     __device__ __forceinline__ double* a11() const { return base + 3 * n(); }         // n()
     __device__ __forceinline__ double* a21() const { return base + 4 * n(); }         // n()
     __device__ __forceinline__ double* bb() const { return base + 5 * n(); }          // n()
-    __device__ __forceinline__ double* Phi() const { return base + (kSlim ? 3 : 6) * n(); }   // 4N Phi_i (2x2 col-major)
+    __device__ __forceinline__ double* Phi() const { return base + (kSlim ? 3 + kAB : 6) * n(); }   // 4N Phi_i (2x2 col-major)
     __device__ __forceinline__ double* Lam() const { return base + 10 * n(); }        // 2N
-    __device__ __forceinline__ double* e() const { return base + (kSlim ? 5 : 12) * n(); }    // 2N free response
+    __device__ __forceinline__ double* e() const { return base + (kSlim ? 5 + kAB : 12) * n(); }    // 2N free response
     // Gamma, block-lower-triangular and packed by column: column j holds rows 2j..2N-1
-    __device__ __forceinline__ double* Gt() const { return base + (kSlim ? 7 : 14) * n(); }   // n()(n()+1)
+    __device__ __forceinline__ double* Gt() const { return base + (kSlim ? 7 + kAB : 14) * n(); }   // n()(n()+1)
     __device__ __forceinline__ int gidx(int r, int j) const { return j * (2 * n() - j + 1) + r - 2 * j; }
     __device__ __forceinline__ double& gt(int r, int j) const { return Gt()[gidx(r, j)]; }   // r >= 2j
     __device__ __forceinline__ double* J() const {                                   // n() x ldj() row-major
@@ -628,17 +635,22 @@ __host__ __device__ constexpr int far_doubles(int N) {
 __host__ __device__ constexpr int ws_doubles(int N, bool far = false) {
     // LDS: the E block (far), or J, R and (N <= kMaxNT) T
     const int jr = far ? (N * (N + 1)) / 2 + (N + 1) : (N <= kMaxNT ? 2 : 1) * N * ldj_of(N) + (N + 1) * ldj_of(N);
-    return ws_slim(N, far) ? 7 * N + N * (N + 1) + jr + 18 * N + 6 : 14 * N + N * (N + 1) + jr + 24 * N + 6;
+    return ws_slim(N, far) ? (7 + slim_ab(N, far)) * N + N * (N + 1) + jr + 18 * N + 6
+                           : 14 * N + N * (N + 1) + jr + 24 * N + 6;
 }
 // workspace bytes with room for `rows` active-row flags: the structured rows of
 // the MPC step are at most 8N+2 (getWLc 6N+4 plus 2(N-1) rate rows); a dense
 // quadprog problem (k_qp) may carry more
 __host__ __device__ constexpr int ws_bytes_rows(int N, int rows, bool far = false) {
-    const int flags = rows > 8 * N + 4 ? rows : 8 * N + 4;
+    const int fmin = slim_ab(N, far) ? 6 * N + 4 : 8 * N + 4;      // (slim_ab: no rate rows)
+    const int flags = rows > fmin ? rows : fmin;
     int b = ws_doubles(N, far) * 8 + 6 * (N + 1) * 4 + N + flags;   // ..., fx (N), aflag
     return (b + 15) & ~15;
 }
-__host__ __device__ constexpr int ws_bytes(int N, bool far = false) { return ws_bytes_rows(N, 8 * N + 4, far); }
+__host__ __device__ constexpr int ws_bytes(int N, bool far = false) {
+    return ws_bytes_rows(N, slim_ab(N, far) ? 6 * N + 4 : 8 * N + 4, far);
+}
+static_assert(!ws_slim(20, true) || 16 * ws_bytes(20, true) <= 160 * 1024, "slim N = 20: 16 scenarios per CU");
 
 // s: the scenario's index in the launch (its far block, when the WS has one)
 template <int NN, bool GEN = false, bool FAR = ws_far(NN)>
@@ -962,7 +974,9 @@ __device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l, do
             ra = coef_a11(k, w.rho()[3 * l]);
             rc = coef_a21(k, w.rho()[3 * l + 1]);
             rbb = coef_b(k, w.rho()[3 * l + 2]);
+            if constexpr (W::kAB) { w.a11()[l] = ra; w.a21()[l] = rc; }
         }
+        if constexpr (W::kAB) NTM_WSYNC();
         const double a0 = gbcast<P>(ra, 0), c0v = gbcast<P>(rc, 0);
         NTM_T0(tlf);
         if (l <= N) {
@@ -980,9 +994,15 @@ __device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l, do
 #pragma unroll
                 for (int u = 0; u < CH; ++u) {
                     const int i = i0 + u;
-                    ca[u] = i < N ? gbcast<P>(ra, i) : 0.0;
-                    cb[u] = i < N ? gbcast<P>(rc, i) : 0.0;
+                    if constexpr (W::kAB) {
+                        ca[u] = i < N ? w.a11()[i] : 0.0;
+                        cb[u] = i < N ? w.a21()[i] : 0.0;
+                    } else {
+                        ca[u] = i < N ? gbcast<P>(ra, i) : 0.0;
+                        cb[u] = i < N ? gbcast<P>(rc, i) : 0.0;
+                    }
                 }
+                if constexpr (W::kAB) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int u = 0; u < CH; ++u) {
                     const int i = i0 + u;

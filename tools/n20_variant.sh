@@ -1,5 +1,7 @@
 # Fast A/B variant of the N = 20 far translation unit only: compiles csrc/ntm_n20.hip
-# with extra flags and links it with the product's other objects (lib/obj/):
+# with extra flags and links it with the product's other objects (lib/obj/).  Only for
+# changes that leave the host side alone (ws_bytes, far_doubles, launch settings):
+# a layout change needs `make variant` (the launches size the LDS from the host TU)
 #   bash tools/n20_variant.sh NAME "-DNTM_N20_CH=4 ..."   ->  lib/libntm_mpc_NAME.so
 set -e
 cd "$(dirname "$0")/../mpc-ntm-control_amd"
