@@ -109,9 +109,9 @@ const char* ntm_last_error(const ntm_ctx* ctx);
 int ntm_ctx_set_stats(ntm_ctx* ctx, int32_t* dev_stats);
 /* Workspace layout of the N = 20 step/run kernels by batch size: batches of at
  * most max_scenarios run on the all-LDS build (2 waves per SIMD), larger ones on
- * the far-workspace build (3 waves per SIMD, GI factors in a per-scenario HBM
- * block).  Default (and max_scenarios < 0): 32 x the device's compute units, the
- * measured crossover (8192 on an MI355X); 0 = always the far build.  Results of
+ * the far-workspace build (4 waves per SIMD, GI factors in a per-scenario HBM
+ * block).  Default (and max_scenarios < 0): 8 x the device's compute units, the
+ * measured crossover (2048 on an MI355X); 0 = always the far build.  Results of
  * the two builds agree to the parity tolerances, not bit for bit; within one
  * build a scenario's results do not depend on the batch around it. */
 int ntm_ctx_set_small_batch(ntm_ctx* ctx, int64_t max_scenarios);

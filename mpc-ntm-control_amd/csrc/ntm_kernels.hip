@@ -400,7 +400,7 @@ struct ntm_ctx {
     size_t fbuf_bytes = 0;
     hipEvent_t fbuf_done = nullptr;   // recorded after the last launch that used fbuf
     int cus = 256;                    // compute units of the device (small_batch)
-    int64_t near_max = -1;            // ntm_ctx_set_small_batch (< 0: 32 x cus)
+    int64_t near_max = -1;            // ntm_ctx_set_small_batch (< 0: 8 x cus)
     hipStream_t stream = nullptr;
 };
 
@@ -501,18 +501,20 @@ int far_release(ntm_ctx* ctx, int rc, hipStream_t st) {
 }
 
 
-// N = 20 batches up to 32 scenarios per CU (four rounds of the all-LDS 2-wave
-// build, which holds 8 per CU at once) run on that build: each of its waves is
-// faster than the far 3-wave build's, whose extra occupancy such a batch cannot
-// use for long (measured, steps 6-25, mode 2: B = 1024 0.74 vs 0.92 ms, 8192 1.49
-// vs 1.51, 16384 2.41 vs 2.26, 65536 7.94 vs 6.85; BASELINE config 2: B = 1024).
+// N = 20 batches up to 8 scenarios per CU (one round of the all-LDS 2-wave build,
+// which holds 8 per CU at once) run on that build: each of its waves is faster
+// than the far build's, whose occupancy such a batch cannot use.  Round 5 (the
+// slim far build at 4 waves per SIMD, 16 per CU; steps 6-25, mode 2, ms per
+// step-batch, all-LDS / far): B = 2048 0.563 / 0.637, 4096 0.772 / 0.708, 8192
+// 1.157 / 0.990, 16384 1.900 / 1.484; BASELINE config 2 (mode 1, B = 1024) 0.279 /
+// 0.319.  (Round 3, the far build at 3 waves: up to 32 per CU, B = 8192 1.49 vs 1.51.)
 // ntm_ctx_set_small_batch overrides the threshold (0: always the far build).
 template <int NN>
 bool small_batch(const ntm_ctx* ctx, int64_t B) {
     if constexpr (NN != 20 || !ws_far(NN)) {
         return false;
     } else {
-        const int64_t lim = ctx->near_max >= 0 ? ctx->near_max : 32LL * ctx->cus;
+        const int64_t lim = ctx->near_max >= 0 ? ctx->near_max : 8LL * ctx->cus;
         return B <= lim;
     }
 }

@@ -32,7 +32,7 @@ def pin_layout(ctl, total: int, cfg=None) -> str:
     for the whole ``total``-scenario batch, and return it ("lds" or "far").
 
     The library chooses the N = 20 build from each call's batch size
-    (ntm_ctx_set_small_batch; all-LDS up to 32 scenarios per CU, the far
+    (ntm_ctx_set_small_batch; all-LDS up to 8 scenarios per CU, the far
     workspace above), so without this a far-build total sharded over many GPUs
     would run its shards on the all-LDS build and lose bitwise agreement with
     the one-GPU run.  Horizons with one build are unaffected."""

@@ -79,13 +79,13 @@ def test_sharded_gather_equals_single_process(tmp_path, world, total):
 
 class _FakeCtl:
     """Stands in for ntm_mpc.NtmMpc: the N = 20 build by batch size (all-LDS up
-    to 8192 scenarios, 32 per CU on 256 CUs) unless pinned."""
+    to 2048 scenarios, 8 per CU on 256 CUs) unless pinned."""
 
     def __init__(self):
         self.limit = -1
 
     def step_layout(self, B, cfg=None):
-        lim = 8192 if self.limit < 0 else self.limit
+        lim = 2048 if self.limit < 0 else self.limit
         return "lds" if B <= lim else "far"
 
     def set_small_batch(self, n):
@@ -96,7 +96,7 @@ def test_pin_layout_follows_the_global_batch():
     """A far-build total sharded into all-LDS-size shards runs every shard on the
     far build (bitwise shard invariance needs one build)."""
     from ntm_mpc.dist import pin_layout, shard_range
-    for total, world, want in ((100_000, 16, "far"), (16_384, 4, "far"), (4096, 2, "lds"), (8192, 8, "lds")):
+    for total, world, want in ((100_000, 16, "far"), (16_384, 4, "far"), (4096, 4, "far"), (2048, 2, "lds"), (1024, 8, "lds")):
         ctl = _FakeCtl()
         assert pin_layout(ctl, total) == want
         for r in range(world):

@@ -250,10 +250,10 @@ def test_run_closed_loop_input_weight(ctl):
     _assert_run_close(out, ref, cfg, k_sim, tol=RUN_TOL, x0=x0, ocfg=ocfg)
 
 
-# N = 20 has two builds (ntm_ctx_set_small_batch): batches up to 32 x the compute
-# units (8192 on an MI355X) run on the all-LDS 2-wave build, which is what the
+# N = 20 has two builds (ntm_ctx_set_small_batch): batches up to 8 x the compute
+# units (2048 on an MI355X) run on the all-LDS 2-wave build, which is what the
 # small batches of these tests reach by default; larger ones on the far-workspace
-# 3-wave build (GI's factors in HBM), forced here.  The full-size tests
+# (slim) 4-wave build (GI's factors in HBM), forced here.  The full-size tests
 # (test_full_size_batch_properties) run the far build at B = 1e5 by default.
 @pytest.mark.parametrize("N,mode,warm", [(20, 1, False), (20, 2, False), (20, 2, True), (20, 3, True)])
 def test_step_teacher_forced_far_build(ctl, N, mode, warm):
@@ -325,12 +325,12 @@ def test_small_batch_builds_agree(ctl):
 
 
 def test_sharded_far_total_is_bitwise(ctl):
-    """A batch that takes the far build on one GPU (16384 > 8192 scenarios),
-    sharded into all-LDS-size shards of 4096 with dist.pin_layout, reproduces
+    """A batch that takes the far build on one GPU (8192 > 2048 scenarios),
+    sharded into all-LDS-size shards of 1024 with dist.pin_layout, reproduces
     the one-GPU batch bit for bit over two closed-loop steps."""
     import ntm_mpc
     from ntm_mpc.dist import pin_layout, shard_range
-    total, world = 16384, 4
+    total, world = 8192, 8
     cfg, _ = cfgs(20, 2)
     x0 = ntm_mpc.scenarios_x0(0, total)
 
