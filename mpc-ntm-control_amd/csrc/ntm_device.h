@@ -453,13 +453,23 @@ __host__ __device__ constexpr bool ws_far(int NN) { return NN > 32 || (NTM_FAR_N
 #ifndef NTM_SLIM20
 #define NTM_SLIM20 1
 #endif
-__host__ __device__ constexpr bool ws_slim(int N, bool far) { return NTM_SLIM20 && far && N == 20; }
+#ifndef NTM_SLIM50
+#define NTM_SLIM50 1
+#endif
+// The slim N = 50 layout (round 5): 4 scenarios per CU (one wave on each SIMD) instead
+// of 3, <= 40,960 B each.  Besides the N = 20 slim changes (its Om is general: the
+// certificate's Om y goes to the 2N of scratch), rho, U_old and the two carried
+// active sets move to the far block (touched once or twice per LPV iteration).
+__host__ __device__ constexpr bool ws_slim(int N, bool far) {
+    return far && ((NTM_SLIM20 && N == 20) || (NTM_SLIM50 && N == 50));
+}
+__host__ __device__ constexpr bool slim_far(int N, bool far) { return ws_slim(N, far) && N == 50; }
 // NTM_SLIM_AB: the slim layout keeps a11 / a21 in LDS after all (2N doubles, paid for by
 // active-row flags for the 6N+4 getWLc rows only: mode 3 never runs on these kernels)
 #ifndef NTM_SLIM_AB
 #define NTM_SLIM_AB 1
 #endif
-__host__ __device__ constexpr int slim_ab(int N, bool far) { return ws_slim(N, far) && NTM_SLIM_AB ? 2 : 0; }
+__host__ __device__ constexpr int slim_ab(int N, bool far) { return NTM_SLIM_AB && N == 20 && ws_slim(N, far) ? 2 : 0; }
 
 template <int NN, bool GEN = false, bool FAR = ws_far(NN)>
 struct WS {
@@ -475,7 +485,9 @@ struct WS {
     __device__ __forceinline__ int ldg() const { return 2 * n(); }
     // double offsets of each array (n() is launch-uniform, so these fold to scalar math)
     static constexpr int kAB = slim_ab(NN, FAR);           // kSlim: a11 / a21 (N each) in LDS
-    __device__ __forceinline__ int oJ() const { return (kSlim ? 7 + kAB : 14) * n() + n() * (n() + 1); }
+    static constexpr bool kSF = slim_far(NN, FAR);          // rho, U_old, cand in the far block
+    static constexpr int kRL = kSF ? 0 : 3;                 // kSlim: rho's N-vectors in LDS
+    __device__ __forceinline__ int oJ() const { return (kSlim ? kRL + 4 + kAB : 14) * n() + n() * (n() + 1); }
     __device__ __forceinline__ int oR() const { return oJ() + n() * ldj(); }
     // T = R^{-1} is kept for N <= kMaxNT only: at long horizons its N^2 doubles would
     // halve the scenarios per CU, and the dual direction falls back to back substitution.
@@ -489,16 +501,19 @@ struct WS {
         if constexpr (kFar) return oJ() + (n() * (n() + 1)) / 2 + (n() + 1);
         else return oT() + (useT() ? n() * ldj() : 0);   // vector block
     }
-    __device__ __forceinline__ double* rho() const { return base; }                 // 3N (3xN col-major)
+    __device__ __forceinline__ double* rho() const {                                  // 3N (3xN col-major)
+        if constexpr (kSF) return far + n() * ldj() + (n() + 1) * ldj() + 3 * n();
+        else return base;
+    }
     // (kSlim: no a11 / a21 / bb / Lam, Phi is 2N of scratch; never called there)
     __device__ __forceinline__ double* a11() const { return base + 3 * n(); }         // n()
     __device__ __forceinline__ double* a21() const { return base + 4 * n(); }         // n()
     __device__ __forceinline__ double* bb() const { return base + 5 * n(); }          // n()
-    __device__ __forceinline__ double* Phi() const { return base + (kSlim ? 3 + kAB : 6) * n(); }   // 4N Phi_i (2x2 col-major)
+    __device__ __forceinline__ double* Phi() const { return base + (kSlim ? kRL + kAB : 6) * n(); }   // 4N Phi_i (2x2 col-major)
     __device__ __forceinline__ double* Lam() const { return base + 10 * n(); }        // 2N
-    __device__ __forceinline__ double* e() const { return base + (kSlim ? 5 + kAB : 12) * n(); }    // 2N free response
+    __device__ __forceinline__ double* e() const { return base + (kSlim ? kRL + 2 + kAB : 12) * n(); }    // 2N free response
     // Gamma, block-lower-triangular and packed by column: column j holds rows 2j..2N-1
-    __device__ __forceinline__ double* Gt() const { return base + (kSlim ? 7 + kAB : 14) * n(); }   // n()(n()+1)
+    __device__ __forceinline__ double* Gt() const { return base + (kSlim ? kRL + 4 + kAB : 14) * n(); }   // n()(n()+1)
     __device__ __forceinline__ int gidx(int r, int j) const { return j * (2 * n() - j + 1) + r - 2 * j; }
     __device__ __forceinline__ double& gt(int r, int j) const { return Gt()[gidx(r, j)]; }   // r >= 2j
     __device__ __forceinline__ double* J() const {                                   // n() x ldj() row-major
@@ -596,10 +611,14 @@ struct WS {
     __device__ __forceinline__ double* uu() const { return base + oV() + (kRi + 8) * n(); }  // n()+1 multipliers
     __device__ __forceinline__ double* xp() const { return base + oV() + (kRi + 9) * n() + 1; }    // 2(n()+1) rollout
     __device__ __forceinline__ double* U() const { return base + oV() + (kRi + 11) * n() + 3; }    // n()
-    __device__ __forceinline__ double* Uold() const { return base + oV() + (kRi + 12) * n() + 3; } // n()
-    __device__ __forceinline__ double* dr() const { return base + oV() + (kRi + 13) * n() + 3; }    // N: d masked to b < q (GI)
-    __device__ __forceinline__ double* irn() const { return base + oV() + (kRi + 14) * n() + 3; }   // 2N: 1/rn_r (0: const row)
-    __device__ __forceinline__ double* ssg() const { return base + oV() + (kRi + 16) * n() + 3; }   // N: sign of general row s
+    static constexpr int kUo = kSF ? 0 : 1;                  // U_old's N-vector in LDS
+    __device__ __forceinline__ double* Uold() const {                                              // n()
+        if constexpr (kSF) return rho() + 3 * n();
+        else return base + oV() + (kRi + 12) * n() + 3;
+    }
+    __device__ __forceinline__ double* dr() const { return base + oV() + (kRi + 12 + kUo) * n() + 3; }    // N: d masked to b < q (GI)
+    __device__ __forceinline__ double* irn() const { return base + oV() + (kRi + 13 + kUo) * n() + 3; }   // 2N: 1/rn_r (0: const row)
+    __device__ __forceinline__ double* ssg() const { return base + oV() + (kRi + 15 + kUo) * n() + 3; }   // N: sign of general row s
     // per-QP constants hoisted out of the solver loops (not kSlim: recomputed from D)
     __device__ __forceinline__ double* vlo() const { return base + oV() + (kRi + 17) * n() + 3; }   // N: umin/D_j
     __device__ __forceinline__ double* vhi() const { return base + oV() + (kRi + 18) * n() + 3; }   // N: umax/D_j
@@ -613,16 +632,20 @@ struct WS {
         if constexpr (kSlim) return ldi() + 2 * n();
         else return base + oV() + (kRi + 21) * n() + 3;
     }
-    static constexpr int kVec = kSlim ? 18 : 24;             // N-vectors of the block (+ 3 + 3 scn)
+    static constexpr int kVec = kSlim ? 17 + kUo : 24;        // N-vectors of the block (+ 3 + 3 scn)
     // this scenario's C1, B.m gain and w_dep (scenario generator; read only when pb.g.phys_on)
     __device__ __forceinline__ double* scn() const { return base + oV() + kVec * n() + 3; }
     __device__ __forceinline__ int* act() const { return reinterpret_cast<int*>(base + oV() + kVec * n() + 6); }
     __device__ __forceinline__ int* sidx() const { return act() + n() + 1; }
-    __device__ __forceinline__ int* cand() const { return act() + 2 * (n() + 1); }   // 2(n()+1): last two active sets
-    __device__ __forceinline__ int* fidx() const { return act() + 4 * (n() + 1); }   // n()+1: free variables (polish)
-    __device__ __forceinline__ int* srw() const { return act() + 5 * (n() + 1); }    // n()+1: state row of general row s
+    static constexpr int kCL = kSF ? 0 : 2;                  // the carried sets' (N+1)-int tables in LDS
+    __device__ __forceinline__ int* cand() const {                                   // 2(n()+1): last two active sets
+        if constexpr (kSF) return reinterpret_cast<int*>(Uold() + n());
+        else return act() + 2 * (n() + 1);
+    }
+    __device__ __forceinline__ int* fidx() const { return act() + (2 + kCL) * (n() + 1); }   // n()+1: free variables (polish)
+    __device__ __forceinline__ int* srw() const { return act() + (3 + kCL) * (n() + 1); }    // n()+1: state row of general row s
     __device__ __forceinline__ unsigned char* fx() const {
-        return reinterpret_cast<unsigned char*>(act() + 6 * (n() + 1));
+        return reinterpret_cast<unsigned char*>(act() + (4 + kCL) * (n() + 1));
     }
     __device__ __forceinline__ unsigned char* aflag() const { return fx() + n(); }
 };
@@ -630,12 +653,15 @@ struct WS {
 __host__ __device__ constexpr int ldj_of(int N) { return N | 1; }
 // the J/R block of a far layout, in HBM per scenario (no T: WS::useT)
 __host__ __device__ constexpr int far_doubles(int N) {
-    return N * ldj_of(N) + (N + 1) * ldj_of(N) + (ws_slim(N, true) ? 3 * N : 0);   // + ldi, kdi, idun (slim)
+    // + ldi, kdi, idun (slim); + rho, U_old and the carried sets' 2(N+1) ints (slim_far)
+    return N * ldj_of(N) + (N + 1) * ldj_of(N) + (ws_slim(N, true) ? 3 * N : 0) +
+           (slim_far(N, true) ? 4 * N + (N + 1) : 0);
 }
 __host__ __device__ constexpr int ws_doubles(int N, bool far = false) {
     // LDS: the E block (far), or J, R and (N <= kMaxNT) T
     const int jr = far ? (N * (N + 1)) / 2 + (N + 1) : (N <= kMaxNT ? 2 : 1) * N * ldj_of(N) + (N + 1) * ldj_of(N);
-    return ws_slim(N, far) ? (7 + slim_ab(N, far)) * N + N * (N + 1) + jr + 18 * N + 6
+    const int rl = slim_far(N, far) ? 0 : 3, uo = slim_far(N, far) ? 0 : 1;
+    return ws_slim(N, far) ? (rl + 4 + slim_ab(N, far)) * N + N * (N + 1) + jr + (17 + uo) * N + 6
                            : 14 * N + N * (N + 1) + jr + 24 * N + 6;
 }
 // workspace bytes with room for `rows` active-row flags: the structured rows of
@@ -644,13 +670,14 @@ __host__ __device__ constexpr int ws_doubles(int N, bool far = false) {
 __host__ __device__ constexpr int ws_bytes_rows(int N, int rows, bool far = false) {
     const int fmin = slim_ab(N, far) ? 6 * N + 4 : 8 * N + 4;      // (slim_ab: no rate rows)
     const int flags = rows > fmin ? rows : fmin;
-    int b = ws_doubles(N, far) * 8 + 6 * (N + 1) * 4 + N + flags;   // ..., fx (N), aflag
+    int b = ws_doubles(N, far) * 8 + (slim_far(N, far) ? 4 : 6) * (N + 1) * 4 + N + flags;   // ..., fx (N), aflag
     return (b + 15) & ~15;
 }
 __host__ __device__ constexpr int ws_bytes(int N, bool far = false) {
     return ws_bytes_rows(N, slim_ab(N, far) ? 6 * N + 4 : 8 * N + 4, far);
 }
 static_assert(!ws_slim(20, true) || 16 * ws_bytes(20, true) <= 160 * 1024, "slim N = 20: 16 scenarios per CU");
+static_assert(!ws_slim(50, true) || 4 * ws_bytes(50, true) <= 160 * 1024, "slim N = 50: 4 scenarios per CU");
 
 // s: the scenario's index in the launch (its far block, when the WS has one)
 template <int NN, bool GEN = false, bool FAR = ws_far(NN)>
@@ -3224,13 +3251,13 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         // below uses its first nS entries, the refinement its first nt <= 2N): y
         // itself stays in w.xp(), where the rollout of a certified U reads it
         // (kSlim: Om = I, so Om y is y itself, read from w.xp())
-        static_assert(!W::kSlim || qi_on<W>(), "the slim layout needs Q = I (qi_on)");
-        double* const omy = W::kSlim ? w.xp() : w.Phi() + 2 * N;
+        constexpr bool kOmyX = W::kSlim && qi_on<W>();     // Om y = y: read w.xp()
+        double* const omy = kOmyX ? w.xp() : (W::kSlim ? w.Phi() : w.Phi() + 2 * N);
         double res = 0.0;
         if (dir) {                                         // n_p in place of the gradient
             if (l < N) res = -((rows.lin(w, dir_p, l) * w.D()[l]) / rows.rnorm(w, dir_p));
         } else {
-        if (l < N && !W::kSlim) {
+        if (l < N && !kOmyX) {
             const double y0 = w.xp()[2 * l], y1 = w.xp()[2 * l + 1];
             omy[2 * l] = om.o0(y0, y1);
             omy[2 * l + 1] = om.o1(y0, y1);
