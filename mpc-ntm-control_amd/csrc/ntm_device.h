@@ -207,7 +207,11 @@ constexpr int kRepairs = NTM_REPAIRS;
 #ifndef NTM_CDP_EXTRA
 #define NTM_CDP_EXTRA 8
 #endif
-constexpr int kCdpExtra = NTM_CDP_EXTRA;   // also at N = 50: 16 / 32 were no faster in mode 2, 6% / 10% slower in mode 3
+constexpr int kCdpExtra = NTM_CDP_EXTRA;
+#ifndef NTM_BOX_REPAIRS
+#define NTM_BOX_REPAIRS 16
+#endif
+constexpr int kBoxRepairs = NTM_BOX_REPAIRS;   // box-only QPs: single-row exchanges before GI (qp_phase)   // also at N = 50: 16 / 32 were no faster in mode 2, 6% / 10% slower in mode 3
 // A constant row (Lin_i = 0: the x_0 rows of getWLc, state rows Gamma doesn't
 // reach) is violated when b_i < -kConstTol (D22, oracle CONST_ROW_TOL): the same
 // absolute 1e-9 the KKT certificate allows on a unit-scale row.  An exact test
@@ -3820,7 +3824,49 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                             qs = cq;
                             continue;
                         }
-                        stage = 1;
+                        stage = pb.mode == NTM_MODE_BOX ? 4 : 1;
+                    }
+                    if (stage == 4) {
+                        // Box-only QPs (BASELINE config 2): single-row exchanges, as before round
+                        // 5.  A violated bound joins (with a negative multiplier too, that row
+                        // leaves in the same exchange; in a full set it takes the place of the
+                        // smallest multiplier); a negative multiplier alone leaves.  Measured on
+                        // the all-LDS build at B = 1024 (one wave per SIMD: the longest scenario
+                        // decides): 0.281 ms per step with the dual path, 0.262 with 8 exchanges,
+                        // 0.224 with 16 (A/B on one box)
+                        if (oks) { okc = true; break; }
+                        if (fk == 3 || nres > kBoxRepairs) { NTM_CNT(CN_CDPX_BUDGET); break; }
+                        if (fk == 1) {
+                            double ud = 0.0;
+                            drop_at(fp, ud);
+                        } else {
+                            if (l < cq) w.aflag()[w.act()[l]] = kActiveRow;
+                            NTM_WSYNC();
+                            const double vmx = fmax(1.0, gmax<P>(l < N ? fabs(vf) : 0.0));
+                            const Pick pk = rows.template check<P>(w, vf, l, false, vmx, w.xp());
+                            NTM_WSYNC();
+                            if (l < cq) w.aflag()[w.act()[l]] = 0;
+                            NTM_WSYNC();
+                            if (pk.p < 0) break;
+                            const int lane = threadIdx.x & 63;
+                            const unsigned long long gm = (P == 64) ? ~0ull : (((1ull << P) - 1ull) << (lane & ~(P - 1)));
+                            const bool keep = l < cq && !(fk == 4 && l == fp);
+                            const unsigned long long km = __ballot(keep) & gm;
+                            const int nkeep = uni<P>((int)__popcll(km));
+                            const int my = (l < cq) ? w.act()[l] : 0;
+                            NTM_WSYNC();
+                            if (nkeep < N) {
+                                if (keep) w.act()[__popcll(km & ((1ull << lane) - 1ull))] = my;
+                                if (l == 0) w.act()[nkeep] = pk.p;
+                                cq = nkeep + 1;
+                            } else if (l == 0) {
+                                w.act()[fp] = pk.p;
+                            }
+                            NTM_WSYNC();
+                        }
+                        qs = cq;
+                        NTM_CNT(CN_CDP_DROP);
+                        continue;
                     }
                     if (stage == 1) {                      // dual feasibility first
                         if (oks) { okc = true; break; }
