@@ -1215,6 +1215,9 @@ typedef double ntm_d4 __attribute__((ext_vector_type(4)));
 #ifndef NTM_MFMA_FF
 #define NTM_MFMA_FF 0      // the re-solve's compact G~_FF (bordered path): measured slower, off
 #endif
+#ifndef NTM_PLANE
+#define NTM_PLANE 1        // k = 2 echelon sets on the null-space path (long horizons, generic kernels)
+#endif
 #ifndef NTM_ROWE_ALL
 #define NTM_ROWE_ALL 0     // 1: the echelon re-solve builds E one sorted row per lane at every horizon
 #endif
@@ -2605,7 +2608,11 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     // makes the rest echelon with k = 1 (the hole as the non-pivot column); the row
     // left out then fixes the step along the null vector instead of the cost.
     constexpr bool kCollision = W::kNN == 0 || W::kNN > 32;
-    if ((kdim == 1 || (kdim == 0 && nS > 0)) && !collide) {
+    // Echelon sets with two spare columns (k = 2, round 5; long horizons): the certified
+    // dual path passes through them after a drop from a k = 1 set; V = V_0 + w1 Z1 + w2 Z2
+    // is minimised over the plane (a 2 x 2 system) instead of the bordered elimination
+    constexpr bool kPlane = kCollision && NTM_PLANE;
+    if ((kdim == 1 || (kdim == 0 && nS > 0) || (kPlane && kdim == 2 && nS > 0)) && !collide) {
         const unsigned long long fm = bal >> (lane & ~(P - 1));   // bit j: variable j is free
         int lastf = -1;
         if (l < nS) {
@@ -2627,10 +2634,16 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         const unsigned long long holes = __ballot(l < nF && colrow[l] < 0) & gmask;
         if ((int)__popcll(holes) == kdim) {                    // every row ends in its own column
             sq = true;
-            nc = kdim ? uni<P>((int)__ffsll((long long)(holes >> (lane & ~(P - 1)))) - 1) : -1;
-            if (l < nS) perm[l] = colrow[l + ((nc >= 0 && l >= nc) ? 1 : 0)];
+            const unsigned long long hg = holes >> (lane & ~(P - 1));
+            nc = kdim ? uni<P>((int)__ffsll((long long)hg) - 1) : -1;
+            if (kPlane && kdim == 2) nc2 = uni<P>((int)__ffsll((long long)(hg & (hg - 1ull))) - 1);
+            if (l < nS) {
+                int c = l + ((nc >= 0 && l >= nc) ? 1 : 0);
+                if (kPlane && nc2 >= 0 && c >= nc2) ++c;
+                perm[l] = colrow[c];
+            }
             NTM_WSYNC();
-        } else if (kCollision && (int)__popcll(holes) == kdim + 1 && (__ballot(l < nS && lastf < 0) & gmask) == 0) {
+        } else if (kCollision && kdim <= 1 && (int)__popcll(holes) == kdim + 1 && (__ballot(l < nS && lastf < 0) & gmask) == 0) {
             // one row does not own its last column (the column's owner is the last writer):
             // k = 0 leaves one hole, k = 1 two (the triangle's spare column and the collision's)
             const unsigned long long orph = __ballot(l < nS && colrow[lastf < 0 ? 0 : lastf] != l) & gmask;
@@ -2877,6 +2890,62 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             ok = b1 != 0.0 && isfinite(b1) && isfinite(b0);
             const double wv = ok ? (hxb - b0) / b1 : 0.0;
             vfin = v0 + wv * zv;
+        } else if (kPlane && ok && nc2 >= 0) {
+            // k = 2: V = V_0 + w1 Z1 + w2 Z2 (Zi = e_{hole i} + Zi_p); with yi = Gamma D Zi
+            // and q = y_0 + e - r the cost is minimised at H w = -g, H_ij = yi' Om yj (+ Ru
+            // dUi' dUj), g_i = yi' Om q (+ Ru dUi' U_0): three Gamma passes, five reductions
+            const double zs2 = __shfl(zz2, (l < N && !fixed) ? rk : 0, P);
+            const double z1 = fixed ? 0.0 : ((fpos == nc) ? 1.0 : (hole ? 0.0 : zs));
+            const double z2 = fixed ? 0.0 : ((fpos == nc2) ? 1.0 : (hole ? 0.0 : zs2));
+            double* const y2s = w.Vb();                       // 2N scratch (Vb, Uf: dead after hs_of)
+            if (l < N) {
+                w.U()[l] = w.D()[l] * v0;
+                w.d()[l] = w.D()[l] * z1;
+                w.dr()[l] = w.D()[l] * z2;
+            }
+            NTM_WSYNC();
+            for (int r = l; r < 2 * N; r += P) {
+                double ya, yb;
+                gamma_row_dot2<NTM_CH>(w, r, w.U(), w.d(), ya, yb);
+                w.xp()[r] = ya;
+                w.Phi()[r] = yb;
+                y2s[r] = gamma_row_dot<NTM_CH>(w, r, w.dr());
+            }
+            NTM_WSYNC();
+            double g1 = 0.0, g2 = 0.0, h11 = 0.0, h12 = 0.0, h22 = 0.0;
+            if (l < N) {
+                const double qa = w.xp()[2 * l] + w.e()[2 * l] - pb.r[0];
+                const double qb = w.xp()[2 * l + 1] + w.e()[2 * l + 1] - pb.r[1];
+                const double aa = w.Phi()[2 * l], ab = w.Phi()[2 * l + 1];
+                const double ca = y2s[2 * l], cb = y2s[2 * l + 1];
+                const double oa = om.o0(aa, ab), ob = om.o1(aa, ab);      // Om y1
+                const double oc = om.o0(ca, cb), od = om.o1(ca, cb);      // Om y2
+                g1 = oa * qa + ob * qb;
+                g2 = oc * qa + od * qb;
+                h11 = oa * aa + ob * ab;
+                h12 = oa * ca + ob * cb;
+                h22 = oc * ca + od * cb;
+                if constexpr (ru_on<W>()) {
+                    const double u0 = w.U()[l], d1 = w.d()[l], d2 = w.dr()[l];
+                    g1 += pb.Ru * (d1 * u0);
+                    g2 += pb.Ru * (d2 * u0);
+                    h11 += pb.Ru * (d1 * d1);
+                    h12 += pb.Ru * (d1 * d2);
+                    h22 += pb.Ru * (d2 * d2);
+                }
+            }
+            g1 = gsum<P>(g1);
+            g2 = gsum<P>(g2);
+            h11 = gsum<P>(h11);
+            h12 = gsum<P>(h12);
+            h22 = gsum<P>(h22);
+            const double det = h11 * h22 - h12 * h12;
+            ok = det > 0.0 && h11 > 0.0 && det < kInf && isfinite(g1) && isfinite(g2);
+            const double w1 = ok ? -((h22 * g1 - h12 * g2) / det) : 0.0;
+            const double w2 = ok ? -((h11 * g2 - h12 * g1) / det) : 0.0;
+            vfin = v0 + w1 * z1 + w2 * z2;
+            for (int r = l; r < 2 * N; r += P) w.xp()[r] += w1 * w.Phi()[r] + w2 * y2s[r];   // y
+            y_ready = true;
         } else if (ok && nc >= 0) {
             zline = fixed ? 0.0 : ((fpos == nc) ? 1.0 : zs);
             line = true;
@@ -3896,13 +3965,21 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                         int li = l;
                         gargmin<P>(th, li);
                         if (!(th < kInf)) {                // full step: p joins A
+                            if (fk != 2) {
+                                // p's own multiplier < 0 at the end point (A's are all >= 0): p
+                                // (nearly) depends on A, an ill-conditioned step at long horizons.
+                                // GI would take its dual-only step there; so does the path (A, V0
+                                // and u0 unchanged).  Dropping that multiplier and continuing
+                                // instead measured slower (config 5 mode 2: 112 -> 156 ms)
+                                NTM_CNT(CN_CDPX_FULLDUAL);
+                                dirp = p;
+                                qs = cq;
+                                stage = 3;
+                                continue;
+                            }
                             ++cq;
                             u0 = (l < cq) ? u1 : 0.0;
                             V0 = vf;
-                            // a negative multiplier at the end point now (p's own: an ill-conditioned
-                            // step at long horizons) goes to GI; dropping it and continuing measured
-                            // slower (config 5 mode 2: 112 -> 156 ms per step-batch, A/B on one box)
-                            if (fk != 2) { NTM_CNT(CN_CDPX_FULLDUAL); break; }
                             pick = true;
                         } else {                           // partial step: row li reaches u = 0 and leaves
                             V0 += th * (vf - V0);
