@@ -12,7 +12,7 @@ from pathlib import Path
 
 outdir, tag = Path(sys.argv[1]), sys.argv[2]
 # resident waves per SIMD of the measured build (N=20: 3 since the far workspace, round 3; 2 before)
-wps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+wps = int(sys.argv[3]) if len(sys.argv) > 3 else 4   # N = 20 slim layout: 4 waves per SIMD (round 5)
 
 
 def last_step(path):
