@@ -180,15 +180,19 @@ def _run_leg(ctl, cfg, B, K, W, x0, rank, world, gen=None, collect=False, stats_
     for i in range(W):
         x = one_step(i, x)["x_next"].clone()
     N = cfg.N
-    hist = None
+    hist = raw = None
     if collect:
-        hist = {"uk": torch.empty(K, B, dtype=torch.float64, device=dev),
-                "Uk": torch.empty(K, N, B, dtype=torch.float64, device=dev),
-                "xk": torch.empty(K + 1, 2, B, dtype=torch.float64, device=dev),
-                "wpred": torch.empty(K, N + 1, B, dtype=torch.float64, device=dev),
-                "exitflag": torch.empty(K, B, dtype=torch.int32, device=dev),
-                "inner_iters": torch.empty(K, B, dtype=torch.int32, device=dev)}
-        hist["xk"][0].copy_(x)
+        # The closed-loop record (NTM_MPC_Sim.m:106-131 keeps uk, Uk, xk per step): each
+        # timed step's kernel writes its outputs straight into their slot of the record,
+        # scenario-major as the ABI wants (no copy kernels between steps; uk and wpred
+        # are views of the stored U and x_pred, extracted after the timed region)
+        raw = {"U": torch.empty(K, B, N, dtype=torch.float64, device=dev),
+               "x_pred": torch.empty(K, B, 2 * (N + 1), dtype=torch.float64, device=dev),
+               "x_next": torch.empty(K + 1, B, 2, dtype=torch.float64, device=dev),
+               "exitflag": torch.empty(K, B, dtype=torch.int32, device=dev),
+               "inner_iters": torch.empty(K, B, dtype=torch.int32, device=dev)}
+        raw["x_next"][0].copy_(x.T)
+        x = raw["x_next"][0].T
     stats = torch.zeros(STATS_ROWS, B, dtype=torch.int32, device=dev)
     ctl.set_stats(stats if stats_on else None)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
@@ -198,23 +202,35 @@ def _run_leg(ctl, cfg, B, K, W, x0, rank, world, gen=None, collect=False, stats_
     t0 = time.perf_counter()
     xin = x
     for i in range(K):
+        if collect:
+            outs[(W + i) & 1] = {"U": raw["U"][i].T, "x_pred": raw["x_pred"][i].T, "x_next": raw["x_next"][i + 1].T,
+                                 "exitflag": raw["exitflag"][i], "inner_iters": raw["inner_iters"][i]}
         ev[i][0].record()
         out = one_step(W + i, xin)
         ev[i][1].record()
-        if collect:
-            hist["uk"][i].copy_(out["U"][0])
-            hist["Uk"][i].copy_(out["U"])
-            hist["xk"][i + 1].copy_(out["x_next"])
-            hist["wpred"][i].copy_(out["x_pred"][0::2])
-            hist["exitflag"][i].copy_(out["exitflag"])
-            hist["inner_iters"][i].copy_(out["inner_iters"])
         xin = out["x_next"]
+    if collect:
+        hist = {"raw": raw}
     return {"t0": t0, "ev": ev, "stats": stats, "out": out, "hist": hist}
+
+
+def _histories(leg):
+    """The step kernels' (K, B, E) records as the (..., B) histories uk, Uk, xk, wpred,
+    exitflag, inner_iters (the gather's and the report's layout); idempotent."""
+    h = leg["hist"]
+    if h is not None and "raw" in h:
+        raw = h.pop("raw")
+        h.update({"uk": raw["U"][:, :, 0].contiguous(), "Uk": raw["U"].permute(0, 2, 1).contiguous(),
+                  "xk": raw["x_next"].permute(0, 2, 1).contiguous(),
+                  "wpred": raw["x_pred"][:, :, 0::2].permute(0, 2, 1).contiguous(),
+                  "exitflag": raw["exitflag"], "inner_iters": raw["inner_iters"]})
+    return h
 
 
 def _finish_leg(ctl, leg, K):
     import torch
     torch.cuda.synchronize()
+    _histories(leg)
     ctl.set_stats(None)
     ctl.set_scenarios(None)
     kern_ms = sum(a.elapsed_time(b) for a, b in leg["ev"]) / K
@@ -288,7 +304,7 @@ def main():
     g = None
     if world > 1:
         tot = world * B
-        g = {k: gather_to_root(v.cpu() if rehearsal else v, tot) for k, v in leg["hist"].items()}
+        g = {k: gather_to_root(v.cpu() if rehearsal else v, tot) for k, v in _histories(leg).items()}
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
