@@ -156,7 +156,7 @@ __shared__ int ntm_trace_grp;   // group (of this one-wave block) that owns the 
 // Diagnostic build only (-DNTM_STAMPS): per-phase s_memtime cycle totals,
 // summed over waves into ntm_stamps[] (read with ntm_debug_stamps).  The
 // production library compiles every stamp away.
-#define NTM_NSTAMPS 80
+#define NTM_NSTAMPS 96
 #ifdef NTM_STAMPS
 extern __device__ unsigned long long ntm_stamps[NTM_NSTAMPS];
 __shared__ unsigned long long ntm_lds_stamps[NTM_NSTAMPS];   // per block (= per wave), flushed once
@@ -189,7 +189,8 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        ST_SC_COL, ST_SC_ROW, ST_SC_END, ST_L_COEF, ST_L_LOOP, CN_CYC_HIT, CN_CYC_SKIP,
        CN_FK_DUAL, CN_FK_PRIMAL, CN_FK_SING, CN_FK_BOTH, ST_GI_WARM,
        CN_CDP_DROP, CN_CDP_RES, CN_CDP_PART, CN_CDP_DIR, CN_CDP_GI,
-       CN_CDPX_SING0, CN_CDPX_SING1, CN_CDPX_BUDGET, CN_CDPX_DIR, CN_CDPX_NOVIOL, CN_CDPX_FULLDUAL, CN_CDPX_TINF };
+       CN_CDPX_SING0, CN_CDPX_SING1, CN_CDPX_BUDGET, CN_CDPX_DIR, CN_CDPX_NOVIOL, CN_CDPX_FULLDUAL, CN_CDPX_TINF,
+       CN_BORD_K0, CN_BORD_K1, CN_BORD_K2, CN_BORD_K3, CN_BORD_K4P, CN_SQ_K0, CN_SQ_K1, CN_SQ_K2, CN_SQ_COLL };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 #ifndef NTM_MAX_NT
 #define NTM_MAX_NT 32
@@ -1217,6 +1218,9 @@ typedef double ntm_d4 __attribute__((ext_vector_type(4)));
 #endif
 #ifndef NTM_PLANE
 #define NTM_PLANE 1        // k = 2 echelon sets on the null-space path (long horizons, generic kernels)
+#endif
+#ifndef NTM_COLL2
+#define NTM_COLL2 1        // square sets with two collisions on the null-space path (long horizons, generic)
 #endif
 #ifndef NTM_ROWE_ALL
 #define NTM_ROWE_ALL 0     // 1: the echelon re-solve builds E one sorted row per lane at every horizon
@@ -2600,6 +2604,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     int nc = -1;                                           // k = 1: the non-pivot compact column
     int nc2 = -1;                                          // k = 1 with one collision: the second hole
     int xb = -1;                                           // one collision: the row left out of the triangle
+    int xb2 = -1;                                          // two collisions (k = 0): the second row left out
     const int kdim = nF - nS;
     // Long horizons with rate rows (config 5) mostly give square sets with ONE
     // collision: two general rows (a rate row and a state row of the same stage)
@@ -2612,6 +2617,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     // dual path passes through them after a drop from a k = 1 set; V = V_0 + w1 Z1 + w2 Z2
     // is minimised over the plane (a 2 x 2 system) instead of the bordered elimination
     constexpr bool kPlane = kCollision && NTM_PLANE;
+    constexpr bool kColl2 = kCollision && NTM_COLL2;
     if ((kdim == 1 || (kdim == 0 && nS > 0) || (kPlane && kdim == 2 && nS > 0)) && !collide) {
         const unsigned long long fm = bal >> (lane & ~(P - 1));   // bit j: variable j is free
         int lastf = -1;
@@ -2660,6 +2666,26 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 }
                 NTM_WSYNC();
             }
+        } else if (kColl2 && kdim == 0 && (int)__popcll(holes) == 2 && (__ballot(l < nS && lastf < 0) & gmask) == 0) {
+            // two rows do not own their last columns (square set, two holes): leaving both
+            // out leaves an echelon system with two spare columns, and the two rows left out
+            // fix the step along the plane instead of the cost (round 5, rate rows at N = 50)
+            const unsigned long long orph = __ballot(l < nS && colrow[lastf < 0 ? 0 : lastf] != l) & gmask;
+            if ((int)__popcll(orph) == 2) {
+                sq = true;
+                const unsigned long long hg = holes >> (lane & ~(P - 1));
+                nc = uni<P>((int)__ffsll((long long)hg) - 1);
+                nc2 = uni<P>((int)__ffsll((long long)(hg & (hg - 1ull))) - 1);
+                const unsigned long long og = orph >> (lane & ~(P - 1));
+                xb = uni<P>((int)__ffsll((long long)og) - 1);
+                xb2 = uni<P>((int)__ffsll((long long)(og & (og - 1ull))) - 1);
+                if (l < nS - 2) {
+                    int c = l + (l >= nc ? 1 : 0);
+                    if (c >= nc2) ++c;
+                    perm[l] = colrow[c];
+                }
+                NTM_WSYNC();
+            }
         }
     }
     NTM_ACC(ST_C_SQ, tp);
@@ -2667,6 +2693,20 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         if (fail_kind) *fail_kind = 3;
         return false;
     }
+#ifdef NTM_STAMPS
+    if (!collide) {                                        // which path the set takes, by spare columns
+        if (sq) {
+            if (xb >= 0) NTM_CNT(CN_SQ_COLL);
+            else if (kdim == 0) NTM_CNT(CN_SQ_K0);
+            else if (kdim == 1) NTM_CNT(CN_SQ_K1);
+            else NTM_CNT(CN_SQ_K2);
+        } else if (kdim <= 0) NTM_CNT(CN_BORD_K0);
+        else if (kdim == 1) NTM_CNT(CN_BORD_K1);
+        else if (kdim == 2) NTM_CNT(CN_BORD_K2);
+        else if (kdim == 3) NTM_CNT(CN_BORD_K3);
+        else NTM_CNT(CN_BORD_K4P);
+    }
+#endif
     // --- g_F (lane a = compact index) ---
     double gl = 0.0;
     if (!sq && l < nF) {
@@ -2760,7 +2800,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         // Sorted E over the pivot columns (row t = general row perm[t] ends in pivot
         // column pc(t) = t + (t >= nc); lower triangular, n x n row-major at Lp[t LD + u]),
         // the non-pivot column e_c (k = 1) and h
-        const int n = nS - (xb >= 0 ? 1 : 0);
+        const int n = nS - (xb >= 0 ? 1 : 0) - (xb2 >= 0 ? 1 : 0);
         auto pc = [&](int u) {                                // pivot column of sorted row u
             int c = u + ((nc >= 0 && u >= nc) ? 1 : 0);
             if (kCollision && nc2 >= 0 && c >= nc2) ++c;
@@ -2830,6 +2870,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             if (kCollision && nc2 >= 0 && nc2 < pc(l)) acz2 = -gen_n(perm[l], w.fidx()[nc2]);
         }
         const double hxb = (kCollision && xb >= 0 && !dir) ? hs_of(xb) : 0.0;   // before w.Phi() is reused
+        const double hxb2 = (kColl2 && xb2 >= 0 && !dir) ? hs_of(xb2) : 0.0;
         NTM_WSYNC();
         if (l < n) sq_id = 1.0 / Ep[w.eidx(l, l)];
         NTM_ACC(ST_S_E, tp);
@@ -2869,7 +2910,24 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         // V_p + w Z_d (eliminating the w with the larger |ai|) for the cost to minimise below
         double vline = v0, zline = 0.0;
         bool line = false;
-        if (kCollision && ok && xb >= 0 && nc2 >= 0) {
+        if (kColl2 && ok && xb2 >= 0) {
+            // two collisions: V = V_0 + w1 Z1 + w2 Z2 with the rows left out fixing
+            // [n_B1'Z1 n_B1'Z2; n_B2'Z1 n_B2'Z2] w = [h_B1 - n_B1'V_0; h_B2 - n_B2'V_0]
+            const double zs2 = __shfl(zz2, (l < N && !fixed) ? rk : 0, P);
+            const double z1 = fixed ? 0.0 : ((fpos == nc) ? 1.0 : (hole ? 0.0 : zs));
+            const double z2 = fixed ? 0.0 : ((fpos == nc2) ? 1.0 : (hole ? 0.0 : zs2));
+            const double nb1 = (l < N && !fixed) ? gen_n(xb, l) : 0.0;
+            const double nb2 = (l < N && !fixed) ? gen_n(xb2, l) : 0.0;
+            const double b10 = gsum<P>(nb1 * v0), a11 = gsum<P>(nb1 * z1), a12 = gsum<P>(nb1 * z2);
+            const double b20 = gsum<P>(nb2 * v0), a21 = gsum<P>(nb2 * z1), a22 = gsum<P>(nb2 * z2);
+            const double det = a11 * a22 - a12 * a21;
+            const double scl = fmax(fmax(fabs(a11), fabs(a12)), fmax(fabs(a21), fabs(a22)));
+            ok = isfinite(det) && fabs(det) > 1e-14 * scl * scl && isfinite(b10) && isfinite(b20);
+            const double r1 = hxb - b10, r2 = hxb2 - b20;
+            const double w1 = ok ? (a22 * r1 - a12 * r2) / det : 0.0;
+            const double w2 = ok ? (a11 * r2 - a21 * r1) / det : 0.0;
+            vfin = v0 + w1 * z1 + w2 * z2;
+        } else if (kCollision && ok && xb >= 0 && nc2 >= 0) {
             const double zs2 = __shfl(zz2, (l < N && !fixed) ? rk : 0, P);
             const double z1 = fixed ? 0.0 : ((fpos == nc) ? 1.0 : (hole ? 0.0 : zs));
             const double z2 = fixed ? 0.0 : ((fpos == nc2) ? 1.0 : (hole ? 0.0 : zs2));
@@ -3350,12 +3408,13 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             // sorted order), back substitution; lane t owns row t and grad at f_t
             if (l < N && !fixed) w.d()[fpos] = res;
             NTM_WSYNC();
-            const int n = nS - (xb >= 0 ? 1 : 0);
+            const int n = nS - (xb >= 0 ? 1 : 0) - (xb2 >= 0 ? 1 : 0);
             int pl = l + ((nc >= 0 && l >= nc) ? 1 : 0);             // lane t's pivot column
             if (kCollision && nc2 >= 0 && pl >= nc2) ++pl;
             double acc = (l < n) ? w.d()[pl] : 0.0, mu = 0.0;
             // one collision: a second right-hand side, the left-out row B at the pivot columns
             double acb = (kCollision && xb >= 0 && l < n) ? gen_n(xb, w.fidx()[pl]) : 0.0, mb = 0.0;
+            double acb2 = (kColl2 && xb2 >= 0 && l < n) ? gen_n(xb2, w.fidx()[pl]) : 0.0, mb2 = 0.0;
             for (int u = n - 1; u >= 0; --u) {
                 const double eu = (l < u) ? w.Ep()[w.eidx(u, l)] : 0.0;
                 const double mu_u = gbcast<P>(acc * sq_id, u);
@@ -3366,8 +3425,27 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                     if (l == u) mb = mb_u;
                     acb -= eu * mb_u;
                 }
+                if (kColl2 && xb2 >= 0) {
+                    const double mb2_u = gbcast<P>(acb2 * sq_id, u);
+                    if (l == u) mb2 = mb2_u;
+                    acb2 -= eu * mb2_u;
+                }
             }
-            if (kCollision && xb >= 0) {
+            if (kColl2 && xb2 >= 0) {
+                // mu = a - mu_1 b1 - mu_2 b2; the two hole columns' equations give mu_1, mu_2:
+                // mu_1 (n_B1[h] - E_h' b1) + mu_2 (n_B2[h] - E_h' b2) = grad[h] - E_h' a
+                const double e1 = (l < n && nc < pl) ? gen_n(perm[l], w.fidx()[nc]) : 0.0;
+                const double e2 = (l < n && nc2 < pl) ? gen_n(perm[l], w.fidx()[nc2]) : 0.0;
+                const double sa1 = gsum<P>(e1 * mu), s11 = gsum<P>(e1 * mb), s12 = gsum<P>(e1 * mb2);
+                const double sa2 = gsum<P>(e2 * mu), s21 = gsum<P>(e2 * mb), s22 = gsum<P>(e2 * mb2);
+                const double m11 = gen_n(xb, w.fidx()[nc]) - s11, m12 = gen_n(xb2, w.fidx()[nc]) - s12;
+                const double m21 = gen_n(xb, w.fidx()[nc2]) - s21, m22 = gen_n(xb2, w.fidx()[nc2]) - s22;
+                const double q1 = w.d()[nc] - sa1, q2 = w.d()[nc2] - sa2;
+                const double det = m11 * m22 - m12 * m21;
+                const double mu1 = (m22 * q1 - m12 * q2) / det, mu2 = (m11 * q2 - m21 * q1) / det;
+                mu -= mu1 * mb + mu2 * mb2;
+                if (l == 0) { w.np()[xb] = mu1; w.np()[xb2] = mu2; }
+            } else if (kCollision && xb >= 0) {
                 // mu = a - mu_B b; a hole column's equation gives mu_B (with two holes,
                 // k = 1, the one with the larger pivot; the other holds at the optimum)
                 const double eh = (l < n && nc < pl) ? gen_n(perm[l], w.fidx()[nc]) : 0.0;
@@ -3422,9 +3500,26 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 for (int u = 0; u < CH; ++u) sub += gv[u] * zv[u];
             }
             res += w.D()[l] * sub;
-            if (rows.has_rate())
-                for (int s2 = 0; s2 < nS; ++s2)
-                    if (w.srw()[s2] >= 2 * N) res -= w.np()[s2] * gen_n(s2, l);
+        }
+        if (W::kNN != 20 && rows.has_rate()) {            // (N = 20 with rate rows runs on the generic kernels)
+            // active rate rows (mode 3): row s of input i has normal entries at i and i-1
+            // only, so each scatters mu_s n_s into two per-input slots (scratch: w.Vb() and
+            // w.d(), dead here) and lane l takes its two; one active rate row per input at
+            // most (both directions of one input active is singular, rejected above).
+            // Replaces an nS-long loop per lane (config 5 mode 3: k_sub 235K cycles per
+            // wave-step)
+            double* const rhi = w.Vb();
+            double* const rlo = w.d();
+            if (l < N) { rhi[l] = 0.0; rlo[l] = 0.0; }
+            NTM_WSYNC();
+            if (l < nS && w.srw()[l] >= 2 * N) {
+                const int i = w.srw()[l] - 2 * N;
+                const double m = w.np()[l];
+                rhi[i] = m * gen_n(l, i);
+                rlo[i - 1] = m * gen_n(l, i - 1);
+            }
+            NTM_WSYNC();
+            if (l < N) res -= rhi[l] + rlo[l];
         }
         NTM_ACC(ST_K_SUB, tp);
         if constexpr (kRefine) {
