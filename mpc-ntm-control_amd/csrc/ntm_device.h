@@ -209,6 +209,9 @@ constexpr int kRepairs = NTM_REPAIRS;
 #define NTM_CDP_EXTRA 8
 #endif
 constexpr int kCdpExtra = NTM_CDP_EXTRA;
+#ifndef NTM_CDP_HINT
+#define NTM_CDP_HINT 1
+#endif
 #ifndef NTM_BOX_REPAIRS
 #define NTM_BOX_REPAIRS 16
 #endif
@@ -3769,7 +3772,7 @@ __device__ __forceinline__ void plant_step(const Prob& pb, const Coef& k, double
 // exactly and KKT-certified.
 // ---------------------------------------------------------------------------
 template <int P, class W>
-__device__ __forceinline__ int shifted_into_act(const Prob& pb, const W& w, const int* c, int l) {
+__device__ __forceinline__ int shifted_into_act(const Prob& pb, const W& w, const int* c, int l, bool hint_only = false) {
     const int N = w.n();
     const int lane = threadIdx.x & 63;
     const unsigned long long gmask = (P == 64) ? ~0ull : (((1ull << P) - 1ull) << (lane & ~(P - 1)));
@@ -3794,6 +3797,12 @@ __device__ __forceinline__ int shifted_into_act(const Prob& pb, const W& w, cons
             if (blk >= 2 || (blk == 1 && rr < 2)) nid = id - 6;   // x_1's state rows would become
             if (blk == N - 1 && rr < 2) dup = id;                  // x_0 rows (constant): dropped
         }
+    }
+    if (hint_only) {                                     // flag the shifted rows (kCandRow) instead
+        if (nid >= 0) w.aflag()[nid] = kCandRow;
+        if (dup >= 0) w.aflag()[dup] = kCandRow;
+        NTM_WSYNC();
+        return 0;
     }
     const unsigned long long bk = __ballot(nid >= 0) & gmask;
     const unsigned long long bd = __ballot(dup >= 0) & gmask;
@@ -3954,6 +3963,14 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                 // dual-only direction of row dirp on A.  stage 0: the carried set;
                 // 1: dropping negative multipliers; 2: A + {p}; 3: the direction of p
                 int stage = 0, qs = cq, dirp = -1, p = -1, nres = 0, fk = 0, fp = 0;
+                // iteration 2 at N <= 32 starts from the unshifted carried set; the dual
+                // path then adds violated rows of its receding-horizon shift first
+                // (StructRows::check prefers kCandRow rows).  Offline (tools/repair_study.py,
+                // N = 20 mode 2): 2.67 -> 2.50 re-solves per iteration-2 QP; on the device
+                // 6.45 -> 6.36 ms per step-batch (A/B on one box).  Not for box-only QPs
+                // (their single-row exchanges: config 2 0.206 -> 0.214 ms with it)
+                if (NTM_CDP_HINT && alt && !shift_first && pb.mode != NTM_MODE_BOX)
+                    (void)shifted_into_act<P>(pb, w, cand, l, true);
                 double vf = 0.0, V0 = 0.0, u0 = 0.0;   // V0: lane = variable; u0: lane = active position
                 bool okc = false;
                 for (;;) {
