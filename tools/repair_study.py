@@ -215,7 +215,7 @@ def device_revert(qp, cand, alt_set, budget=8, max_skip=99):
         rep += 1
 
 
-def gi_resolve(qp, cand, alt_set, budget=16, dual_first=True):
+def gi_resolve(qp, cand, alt_set, budget=16, dual_first=True, hint=None):
     """Goldfarb-Idnani's dual path evaluated by certified re-solves: from a dual
     feasible set A (multipliers u0 >= 0 at its equality-constrained optimum V0),
     add the most violated row p: the re-solve on A + {p} is the full step's end
@@ -244,6 +244,10 @@ def gi_resolve(qp, cand, alt_set, budget=16, dual_first=True):
         vmax = max(1.0, np.abs(V0).max())
         if not (sm[p] < -1e-9 * max(vmax, abs(qp.b[p] / qp.rn[p]))):
             return True, n                     # (certified by the last re-solve)
+        if hint is not None:                   # steer: a violated row of the hint set first
+            hv = [i for i in hint if i not in act and sm[i] < -1e-9 * max(vmax, abs(qp.b[i] / qp.rn[i]))]
+            if hv:
+                p = min(hv, key=lambda i: sm[i])
         up = 0.0
         while True:
             A1 = act + [p]
@@ -327,14 +331,14 @@ rho, Uo = cbind.initial_state(x, cfg)
 for _ in range(lo - 2):
     r = cbind.step(x, rho, Uo, cfg)
     x, rho, Uo = r["x_next"], r["rho"], r["U_old"]
+HINTS = {}
 strategies = {
     "device (8 repairs)": lambda q, c, a: device_repair(q, c, a, 8),
-    "device (16 repairs)": lambda q, c, a: device_repair(q, c, a, 16),
-    "GI by re-solves (16)": lambda q, c, a: gi_resolve(q, c, a, 16),
+    "GI: hint shift(prev 10)": lambda q, c, a: gi_resolve(q, c, a, 64, hint=HINTS.get("s10")),
+    "GI: hint prev 2": lambda q, c, a: gi_resolve(q, c, a, 64, hint=HINTS.get("p2")),
+    "GI: hint shift(prev 2)": lambda q, c, a: gi_resolve(q, c, a, 64, hint=HINTS.get("s2")),
+    "GI: hint shift(p10) + shift(p2)": lambda q, c, a: gi_resolve(q, c, a, 64, hint=HINTS.get("u")),
     "GI by re-solves (64)": lambda q, c, a: gi_resolve(q, c, a, 64),
-    "1 repair + GI by re-solves": lambda q, c, a: hybrid(q, c, a, 1),
-    "2 repairs + GI by re-solves": lambda q, c, a: hybrid(q, c, a, 2),
-    "4 repairs + GI by re-solves": lambda q, c, a: hybrid(q, c, a, 4),
 }
 res = {it: {k: [0, 0, 0] for k in strategies} for it in ITERS}   # certified, re-solves, count
 exact = {it: 0 for it in ITERS}
@@ -360,6 +364,11 @@ for s in range(S):
                         continue
                     cand, alt = sets[it - 2], None
                 qp = QP(rc["G"], rc["F"], rc["Lin"], rc["b"])
+                if it == 2 and 2 in prev:
+                    HINTS.update(s10=shift(prev[10]), p2=list(prev[2]), s2=shift(prev[2]),
+                                 u=list(dict.fromkeys(shift(prev[10]) + shift(prev[2]))))
+                else:
+                    HINTS.clear()
                 exact[it] += set(cand) == set(sets[it])
                 first_fail[it] += QP(rc["G"], rc["F"], rc["Lin"], rc["b"]).solve(cand)[0] != 0
                 for name, f in strategies.items():
