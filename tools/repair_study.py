@@ -364,11 +364,15 @@ for s in range(S):
                         continue
                     cand, alt = sets[it - 2], None
                 qp = QP(rc["G"], rc["F"], rc["Lin"], rc["b"])
+                HINTS.clear()
                 if it == 2 and 2 in prev:
                     HINTS.update(s10=shift(prev[10]), p2=list(prev[2]), s2=shift(prev[2]),
                                  u=list(dict.fromkeys(shift(prev[10]) + shift(prev[2]))))
-                else:
-                    HINTS.clear()
+                elif it == 1:
+                    HINTS.update(s10=shift(prev[9]), p2=list(prev[10]), s2=list(prev[1]) if 1 in prev else None)
+                elif it >= 3 and it - 1 in sets:
+                    HINTS.update(s10=list(sets[it - 1]), p2=list(prev[it]) if it in prev else None,
+                                 s2=shift(prev[it]) if it in prev else None)
                 exact[it] += set(cand) == set(sets[it])
                 first_fail[it] += QP(rc["G"], rc["F"], rc["Lin"], rc["b"]).solve(cand)[0] != 0
                 for name, f in strategies.items():
