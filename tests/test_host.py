@@ -166,3 +166,31 @@ def test_product_never_imports_oracle():
     bad = re.compile(r"(import\s+oracle|from\s+oracle|libntm_oracle|cbind|ntm_oracle_)")
     for f in list(pkg.rglob("*.py")) + list(pkg.rglob("*.hip")) + list(pkg.rglob("*.h")) + [pkg / "Makefile"]:
         assert not bad.search(f.read_text()), f
+
+
+def test_bench_record_histories():
+    """bench.py's closed-loop record: the step kernels write scenario-major (K, B, E)
+    slots (each an (E, B) ABI view), and _histories forms the (..., B) histories the
+    gather and the report use: uk = U(1), Uk, xk (with x_0), wpred = x_pred(1:2:end)."""
+    import importlib.util
+    import torch
+    spec = importlib.util.spec_from_file_location("bench_mod", ROOT / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    K, B, N = 3, 5, 4
+    g = torch.Generator().manual_seed(0)
+    raw = {"U": torch.randn(K, B, N, generator=g, dtype=torch.float64),
+           "x_pred": torch.randn(K, B, 2 * (N + 1), generator=g, dtype=torch.float64),
+           "x_next": torch.randn(K + 1, B, 2, generator=g, dtype=torch.float64),
+           "exitflag": torch.ones(K, B, dtype=torch.int32), "inner_iters": torch.full((K, B), 10, dtype=torch.int32)}
+    for i in range(K):                              # the per-step views the kernels write
+        assert raw["U"][i].T.shape == (N, B) and raw["U"][i].T.T.is_contiguous()
+    h = bench._histories({"hist": {"raw": dict(raw)}})
+    assert h["Uk"].shape == (K, N, B) and h["xk"].shape == (K + 1, 2, B) and h["wpred"].shape == (K, N + 1, B)
+    for i in range(K):
+        assert torch.equal(h["uk"][i], raw["U"][i][:, 0])
+        assert torch.equal(h["Uk"][i], raw["U"][i].T)
+        assert torch.equal(h["wpred"][i], raw["x_pred"][i].T[0::2])
+    for i in range(K + 1):
+        assert torch.equal(h["xk"][i], raw["x_next"][i].T)
+    assert bench._histories({"hist": h}) is h       # idempotent
