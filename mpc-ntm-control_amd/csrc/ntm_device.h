@@ -209,6 +209,15 @@ constexpr int kRepairs = NTM_REPAIRS;
 #define NTM_CDP_EXTRA 8
 #endif
 constexpr int kCdpExtra = NTM_CDP_EXTRA;
+#ifndef NTM_SPLIT_SCALE
+#define NTM_SPLIT_SCALE 1
+#endif
+#ifndef NTM_SPLIT_FAR
+#define NTM_SPLIT_FAR 0
+#endif
+#ifndef NTM_SPLIT_PRAGMA
+#define NTM_SPLIT_PRAGMA NTM_CHUNK_PRAGMA
+#endif
 #ifndef NTM_CDP_HINT
 #define NTM_CDP_HINT 1
 #endif
@@ -1375,6 +1384,125 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
     const OmQ<qi_on<W>()> qw(pb.Q);
     int bad = 0;
     NTM_T0(tsc);
+    // Short horizons (2N <= 64, N = 20): the column pass and the row pass each split
+    // their sums in two halves at H = ceil(N/2) on otherwise idle lanes, so the wave
+    // runs H trips instead of N (lanes N..2N-1 take the columns' i >= H terms; lanes
+    // 2N.. the j >= H terms of rows with r >= 2H).  The sums are then (first half) +
+    // (second half) instead of one sequential pass.  The all-LDS build only (config 2,
+    // B = 1024: 0.208 -> 0.199 ms; mode 2 at B = 1024: 0.545 -> 0.526 ms).  The far
+    // build's register allocation does not absorb it: 6.36 -> 7.98 ms per step-batch
+    // at B = 1e5 with the chunk unroll, 6.41 ms without (A/B on one box, NTM_SPLIT_FAR)
+    constexpr int NNs = W::kNN, Hs = (NNs + 1) / 2;
+    constexpr bool kSplit = NTM_SPLIT_SCALE && (NTM_SPLIT_FAR || !W::kFar) && P == 64 && NNs > 0 && 4 * NNs - 2 * Hs <= 64;
+    if constexpr (kSplit) {
+        double s = 0.0, fs = 0.0;
+        const int col = l < N ? l : l - N;
+        const int base = l < N ? 0 : Hs;
+        if (l < 2 * N) {
+            const double* cj = w.Gt() + w.gidx(2 * col, col) - 2 * col;
+            const double* om = w.xp();
+            constexpr int CH = NTM_CH;
+            NTM_SPLIT_PRAGMA
+            for (int u0 = 0; u0 < Hs; u0 += CH) {
+                double ga[CH], gb[CH], ea[CH], eb[CH];
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    const int i = base + u0 + u;
+                    const bool in = u0 + u < Hs && i < N;
+                    ga[u] = in ? cj[2 * i] : 0.0;
+                    gb[u] = in ? cj[2 * i + 1] : 0.0;
+                    ea[u] = in ? om[2 * i] : 0.0;
+                    eb[u] = in ? om[2 * i + 1] : 0.0;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < CH; ++u) {
+                    const int i = base + u0 + u;
+                    const double g0 = ga[u], g1 = gb[u];
+                    const double o0 = qw.o0(g0, g1);
+                    const double o1 = qw.o1(g0, g1);
+                    const double t = g0 * o0 + g1 * o1;
+                    const double tf = g0 * ea[u] + g1 * eb[u];
+                    const bool on = u0 + u < Hs && i >= col && i < N;
+                    if (on) bad |= !isfinite(g0) || !isfinite(g1);
+                    s += on ? t : 0.0;
+                    fs += on ? tf : 0.0;
+                }
+            }
+        }
+        const double s2 = __shfl(s, (l + N) & 63, 64);
+        const double f2 = __shfl(fs, (l + N) & 63, 64);
+        if (l < N) {
+            double g = 2 * (s + s2);
+            if constexpr (ru_on<W>()) g = g + 2 * pb.Ru;   // G_ll + 2 Ru (ABI v5)
+            const double Dl = (g > 0.0 && g < kInf) ? rsqrt_nr(g) : 1.0;
+            w.D()[l] = Dl;
+            const double f = (2 * (fs + f2)) * Dl;
+            bad |= !isfinite(f) || !isfinite(Dl);
+            w.F()[l] = f;
+            if constexpr (!W::kSlim) {
+                w.vlo()[l] = -((-pb.umin) / Dl);
+                w.vhi()[l] = pb.umax / Dl;
+            }
+        }
+        NTM_WSYNC();
+        NTM_ACC(ST_SC_COL, tsc);
+        if (pb.mode == NTM_MODE_FULL_DU && l >= 1 && l < N) {
+            const double a = w.D()[l], b = w.D()[l - 1];
+            w.idun()[l] = 1.0 / sqrt(a * a + b * b);
+        }
+        if (with_state_rows) {
+            const bool lo = l < 2 * N, hi = !lo && l < 4 * N - 2 * Hs;
+            const int r = lo ? l : (hi ? l - 2 * N + 2 * Hs : 0);
+            const int jb = lo ? 0 : Hs;
+            const int jmax = r >> 1;
+            double rs = 0.0;
+            int last = -1, cnt = 0;
+            if (lo || hi) {
+                constexpr int CH = NTM_CH;
+                NTM_SPLIT_PRAGMA
+                for (int u0 = 0; u0 < Hs; u0 += CH) {
+                    double g[CH], dd[CH];
+#pragma unroll
+                    for (int u = 0; u < CH; ++u) {
+                        const int j = jb + u0 + u;
+                        const bool in = u0 + u < Hs && j < N;
+                        g[u] = in ? w.gt(r, j) : 0.0;
+                        dd[u] = in ? w.D()[j] : 0.0;
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int u = 0; u < CH; ++u) {
+                        const int j = jb + u0 + u;
+                        const double v = g[u] * dd[u];
+                        const bool in = u0 + u < Hs && j <= jmax;
+                        rs += in ? v * v : 0.0;
+                        if (in && g[u] != 0.0) { last = j; ++cnt; }
+                    }
+                }
+            }
+            // the row's second half sits on lane 2N + r - 2H (rows r >= 2H)
+            const int src = (l >= 2 * Hs && l < 2 * N) ? l + 2 * N - 2 * Hs : l;
+            const double rs2 = __shfl(rs, src & 63, 64);
+            const int last2 = __shfl(last, src & 63, 64);
+            const int cnt2 = __shfl(cnt, src & 63, 64);
+            if (lo) {
+                const bool two = src != l;
+                const double sr = two ? rs + rs2 : rs;
+                const int lr = (two && last2 >= 0) ? last2 : last;
+                const int cr = two ? cnt + cnt2 : cnt;
+                bad |= !isfinite(sr) || !isfinite(w.e()[r]);
+                const double ir = (sr > 0.0 && sr < kInf) ? rsqrt_nr(sr) : 0.0;
+                w.irn()[r] = ir;
+                w.rinfo()[r] = (lr + 1) | (cr > 1 ? kRowMulti : 0);
+            }
+            NTM_WSYNC();
+        }
+        NTM_ACC(ST_SC_ROW, tsc);
+        const bool ok = gmaxi<P>(bad) == 0;
+        NTM_ACC(ST_SC_END, tsc);
+        return ok;
+    }
     if (l < N) {
         // one pass over Gamma's column l: the Gram diagonal G_ll and F_l = 2 Gamma_l' Om (e - r)
         const double* cj = w.Gt() + w.gidx(2 * l, l) - 2 * l;
