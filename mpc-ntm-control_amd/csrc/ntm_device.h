@@ -1391,24 +1391,29 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
     // (second half) instead of one sequential pass.  The all-LDS build only (config 2,
     // B = 1024: 0.208 -> 0.199 ms; mode 2 at B = 1024: 0.545 -> 0.526 ms).  The far
     // build's register allocation does not absorb it: 6.36 -> 7.98 ms per step-batch
-    // at B = 1e5 with the chunk unroll, 6.41 ms without (A/B on one box, NTM_SPLIT_FAR)
+    // at B = 1e5 with the chunk unroll, 6.41 ms without; the column pass alone 7.11 ms,
+    // the row pass alone 9.66 ms (A/B on one box, NTM_SPLIT_FAR)
     constexpr int NNs = W::kNN, Hs = (NNs + 1) / 2;
-    constexpr bool kSplit = NTM_SPLIT_SCALE && (NTM_SPLIT_FAR || !W::kFar) && P == 64 && NNs > 0 && 4 * NNs - 2 * Hs <= 64;
-    if constexpr (kSplit) {
+    constexpr bool kSplit = NTM_SPLIT_SCALE && P == 64 && NNs > 0 && 4 * NNs - 2 * Hs <= 64;
+    // NTM_SPLIT_FAR (far build): bit 0 the column pass, bit 1 the row pass
+    constexpr bool kSC = kSplit && (!W::kFar || (NTM_SPLIT_FAR & 1));
+    constexpr bool kSR = kSplit && (!W::kFar || (NTM_SPLIT_FAR & 2));
+    constexpr int TC = kSC ? Hs : NNs, TR = kSR ? Hs : NNs;   // trips of each pass
+    if constexpr (kSC || kSR) {
         double s = 0.0, fs = 0.0;
         const int col = l < N ? l : l - N;
         const int base = l < N ? 0 : Hs;
-        if (l < 2 * N) {
+        if (l < (kSC ? 2 * N : N)) {
             const double* cj = w.Gt() + w.gidx(2 * col, col) - 2 * col;
             const double* om = w.xp();
             constexpr int CH = NTM_CH;
             NTM_SPLIT_PRAGMA
-            for (int u0 = 0; u0 < Hs; u0 += CH) {
+            for (int u0 = 0; u0 < TC; u0 += CH) {
                 double ga[CH], gb[CH], ea[CH], eb[CH];
 #pragma unroll
                 for (int u = 0; u < CH; ++u) {
                     const int i = base + u0 + u;
-                    const bool in = u0 + u < Hs && i < N;
+                    const bool in = u0 + u < TC && i < N;
                     ga[u] = in ? cj[2 * i] : 0.0;
                     gb[u] = in ? cj[2 * i + 1] : 0.0;
                     ea[u] = in ? om[2 * i] : 0.0;
@@ -1423,21 +1428,21 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
                     const double o1 = qw.o1(g0, g1);
                     const double t = g0 * o0 + g1 * o1;
                     const double tf = g0 * ea[u] + g1 * eb[u];
-                    const bool on = u0 + u < Hs && i >= col && i < N;
+                    const bool on = u0 + u < TC && i >= col && i < N;
                     if (on) bad |= !isfinite(g0) || !isfinite(g1);
                     s += on ? t : 0.0;
                     fs += on ? tf : 0.0;
                 }
             }
         }
-        const double s2 = __shfl(s, (l + N) & 63, 64);
-        const double f2 = __shfl(fs, (l + N) & 63, 64);
+        const double s2 = kSC ? __shfl(s, (l + N) & 63, 64) : 0.0;
+        const double f2 = kSC ? __shfl(fs, (l + N) & 63, 64) : 0.0;
         if (l < N) {
-            double g = 2 * (s + s2);
+            double g = kSC ? 2 * (s + s2) : 2 * s;
             if constexpr (ru_on<W>()) g = g + 2 * pb.Ru;   // G_ll + 2 Ru (ABI v5)
             const double Dl = (g > 0.0 && g < kInf) ? rsqrt_nr(g) : 1.0;
             w.D()[l] = Dl;
-            const double f = (2 * (fs + f2)) * Dl;
+            const double f = (kSC ? 2 * (fs + f2) : 2 * fs) * Dl;
             bad |= !isfinite(f) || !isfinite(Dl);
             w.F()[l] = f;
             if constexpr (!W::kSlim) {
@@ -1452,7 +1457,7 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
             w.idun()[l] = 1.0 / sqrt(a * a + b * b);
         }
         if (with_state_rows) {
-            const bool lo = l < 2 * N, hi = !lo && l < 4 * N - 2 * Hs;
+            const bool lo = l < 2 * N, hi = kSR && !lo && l < 4 * N - 2 * Hs;
             const int r = lo ? l : (hi ? l - 2 * N + 2 * Hs : 0);
             const int jb = lo ? 0 : Hs;
             const int jmax = r >> 1;
@@ -1461,12 +1466,12 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
             if (lo || hi) {
                 constexpr int CH = NTM_CH;
                 NTM_SPLIT_PRAGMA
-                for (int u0 = 0; u0 < Hs; u0 += CH) {
+                for (int u0 = 0; u0 < TR; u0 += CH) {
                     double g[CH], dd[CH];
 #pragma unroll
                     for (int u = 0; u < CH; ++u) {
                         const int j = jb + u0 + u;
-                        const bool in = u0 + u < Hs && j < N;
+                        const bool in = u0 + u < TR && j < N;
                         g[u] = in ? w.gt(r, j) : 0.0;
                         dd[u] = in ? w.D()[j] : 0.0;
                     }
@@ -1475,17 +1480,17 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
                     for (int u = 0; u < CH; ++u) {
                         const int j = jb + u0 + u;
                         const double v = g[u] * dd[u];
-                        const bool in = u0 + u < Hs && j <= jmax;
+                        const bool in = u0 + u < TR && j <= jmax;
                         rs += in ? v * v : 0.0;
                         if (in && g[u] != 0.0) { last = j; ++cnt; }
                     }
                 }
             }
             // the row's second half sits on lane 2N + r - 2H (rows r >= 2H)
-            const int src = (l >= 2 * Hs && l < 2 * N) ? l + 2 * N - 2 * Hs : l;
-            const double rs2 = __shfl(rs, src & 63, 64);
-            const int last2 = __shfl(last, src & 63, 64);
-            const int cnt2 = __shfl(cnt, src & 63, 64);
+            const int src = (kSR && l >= 2 * Hs && l < 2 * N) ? l + 2 * N - 2 * Hs : l;
+            const double rs2 = kSR ? __shfl(rs, src & 63, 64) : 0.0;
+            const int last2 = kSR ? __shfl(last, src & 63, 64) : -1;
+            const int cnt2 = kSR ? __shfl(cnt, src & 63, 64) : 0;
             if (lo) {
                 const bool two = src != l;
                 const double sr = two ? rs + rs2 : rs;
