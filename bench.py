@@ -13,6 +13,10 @@ gathered over RCCL at the end of the timed region (the end-of-batch gather).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+With --gpus N > 1 and no WORLD_SIZE in the environment, the script starts the
+N ranks itself (torch.distributed.run as a child process, before any GPU
+call); under a launcher, WORLD_SIZE must equal --gpus or it exits with 2.
+
 Rank 0 prints ONE JSON line (bench contract).  roofline.achieved uses this
 build's own algorithmic flop count (ntm_mpc/flops.py),
 driven by the kernel's own solver counters accumulated over exactly the K
@@ -39,7 +43,7 @@ FP64_PEAK_TFLOPS = 78.6     # MI355X dense fp64 (vector = matrix), spec
 HBM_PEAK_GBS = 8000.0
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -60,7 +64,62 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse the multi-rank "
                          "control flow with more ranks than GPUs (ranks share devices, timing not meaningful)")
-    return ap.parse_args()
+    ap.add_argument("--stub-rank", action="store_true",
+                    help="test only: each rank joins a gloo group and reports its rank, no GPU work "
+                         "(exercises the --gpus launcher on a CPU-only host)")
+    return ap.parse_args(argv)
+
+
+def launch_plan(gpus, env):
+    """How this process takes part in a --gpus run (one process per GPU):
+    ("here", None) when it is a rank of a launched job (WORLD_SIZE set and equal
+    to --gpus) or the only process (--gpus 1); ("spawn", n) when it must start
+    n ranks itself; ("error", message) when WORLD_SIZE and --gpus disagree, so a
+    launcher mistake never yields a one-GPU line labelled as a scaling point."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            return "error", f"bench.py: WORLD_SIZE={ws} but --gpus {gpus}"
+        return "here", None
+    if gpus < 1:
+        return "error", f"bench.py: --gpus {gpus}"
+    return ("spawn", gpus) if gpus > 1 else ("here", None)
+
+
+def spawn_ranks(n, argv):
+    """Start n ranks of this script under torch.distributed.run (one node,
+    rendezvous on 127.0.0.1) as a CHILD process and return its exit code.  The
+    caller has made no GPU call (no HIP initialisation in the parent: the
+    ranks own the devices); rank 0's JSON line reaches stdout through the
+    launcher."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # dmabuf IPC only on this pool (RCCL)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def stub_rank(world, rank):
+    """--stub-rank: the rank's part of the launcher test, on CPU (gloo)."""
+    import torch
+    import torch.distributed as dist
+    per_rank = [rank]
+    if world > 1:
+        dist.init_process_group("gloo")
+        allr = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(allr, torch.tensor([rank], dtype=torch.int64))
+        per_rank = [int(t.item()) for t in allr]
+    if rank == 0:
+        print(json.dumps({"stub": True, "n_gpus": world, "per_rank": {"rank": per_rank}}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def _cpu_model():
@@ -265,12 +324,23 @@ def _verify_gathered(ctl, cfg, B_total, K, W, g, n_verify, seed=12345):
 
 def main():
     args = parse()
-    import torch
-    import torch.distributed as dist
-
+    # --gpus N: the driver launches N ranks itself (torch.distributed.run, WORLD_SIZE
+    # set); a bare `python bench.py --gpus N` starts them here, before any GPU call
+    plan, arg = launch_plan(args.gpus, os.environ)
+    if plan == "error":
+        print(arg, file=sys.stderr, flush=True)
+        return 2
+    if plan == "spawn":
+        return spawn_ranks(arg, sys.argv[1:])
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.stub_rank:
+        stub_rank(world, rank)
+        return 0
+    import torch
+    import torch.distributed as dist
+
     rehearsal = args.dist_backend == "gloo"
     if rehearsal:                       # ranks fold onto the available devices
         local = local % max(1, torch.cuda.device_count())
@@ -418,7 +488,8 @@ def main():
     if world > 1:
         dist.barrier()                  # rank 0 may still be timing the CPU baseline
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

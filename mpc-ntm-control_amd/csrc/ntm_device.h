@@ -3954,6 +3954,9 @@ __device__ __forceinline__ int shifted_into_act(const Prob& pb, const W& w, cons
 // own instead of the step kernel's (the caller's live registers are saved around
 // the call); 0 inlines it like every other phase.
 // ---------------------------------------------------------------------------
+#ifndef NTM_GI_DEFER_PROBE
+#define NTM_GI_DEFER_PROBE 0   // probe only: GI and the dual-only direction compiled out
+#endif
 #ifndef NTM_GI_OUTLINE
 #define NTM_GI_OUTLINE 0
 #endif
@@ -4199,6 +4202,7 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                     } else if (stage == 2) {               // the end point of adding p
                         NTM_CNT(CN_CDP_RES);
                         if (oks) { ++cq; okc = true; break; }
+                        if (NTM_GI_DEFER_PROBE && fk == 3) break;
                         if (fk == 3) {                     // A + {p} singular: p depends on A
                             dirp = p;
                             qs = cq;
@@ -4210,6 +4214,7 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                         int li = l;
                         gargmin<P>(th, li);
                         if (!(th < kInf)) {                // full step: p joins A
+                            if (NTM_GI_DEFER_PROBE && fk != 2) break;
                             if (fk != 2) {
                                 // p's own multiplier < 0 at the end point (A's are all >= 0): p
                                 // (nearly) depends on A, an ill-conditioned step at long horizons.
@@ -4256,6 +4261,7 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                         p = pk.p;
                     }
                     if (nres >= budget) { NTM_CNT(CN_CDPX_BUDGET); break; }   // add p: A + {p}, or its direction when A is full
+                    if (NTM_GI_DEFER_PROBE && cq >= N) break;
                     if (cq >= N) {
                         dirp = p;
                         qs = cq;
@@ -4427,7 +4433,12 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
             }
             if (!done) {
                 if (n_girun) ++*n_girun;
+#if NTM_GI_DEFER_PROBE
+                flag = NTM_EXIT_MAXITER;
+                (void)nwarm;
+#else
                 flag = gi_fallback<P, W>(pb, w, rows, nrows, l, nwarm, it, qp_iters, &q, &ns, &yv);
+#endif
             }
         }
     }

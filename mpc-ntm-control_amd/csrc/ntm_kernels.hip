@@ -615,11 +615,12 @@ bool force_generic() {
 // The input weight Ru (ABI v5) is compiled into the generic kernels only (ru_on in
 // ntm_device.h), like D4 / D6: the reference's cost has none (Ru = 0).  So is a
 // stage weight other than the reference's Q = I (NTM_MPC_Sim.m:59; qi_on): the
-// specialised kernels take the identity for Om.
+// specialised kernels up to NTM_QI_MAXN (N = 10, 20) take the identity for Om; the
+// N = 50 kernel keeps a general Om and runs any Q itself.
 bool q_is_identity(const ntm_config* c) { return c->Q[0] == 1.0 && c->Q[1] == 0.0 && c->Q[2] == 0.0 && c->Q[3] == 1.0; }
 bool use_generic(const ntm_config* c) {
     return force_generic() || (c->flags & kGenericOnlyFlags) != 0 || (c->N == 20 && c->mode == NTM_MODE_FULL_DU) ||
-           c->Ru != 0.0 || !q_is_identity(c);
+           c->Ru != 0.0 || (c->N <= NTM_QI_MAXN && !q_is_identity(c));
 }
 #ifdef NTM_RU_ONLY20
 // resource-usage check of the N=20 hot kernel alone (make ru20): every horizon

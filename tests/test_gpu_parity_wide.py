@@ -28,6 +28,18 @@ GOLD = Path(__file__).resolve().parent / "golden"
 # scenarios), injected at every step, so a scenario may drift up to 10 sens[s]
 # (round 4 measured GPU / sens <= 1.8 on the three most sensitive ones).
 SENS_FACTOR = 10.0
+# Only (N = 50, mode 3) needs the sensitivity bound: the other three configs hold
+# RUN_TOL on every scenario (keep their 5e-8, so a regression in the
+# sensitive scenarios cannot pass silently).  For (50, 3) the number of scenarios
+# above RUN_TOL is bounded by the recorded count plus a margin.
+SENS_BOUND = {(50, 3)}
+ABOVE_MAX = {(50, 3): 7 + 3}                   # 7 recorded (rounds 5 and 6)
+# Scenarios whose LPV iteration count or exit flag differs from the oracle's at
+# some step (the bitwise stopping rule), replayed along the GPU's
+# path: the recorded count per config (256 scenarios, 20 steps) plus a margin,
+# instead of a blanket 40%
+DIV_RECORDED = {(20, 2): 0, (20, 3): 0, (50, 2): 0, (50, 3): 0}
+DIV_MARGIN = 8
 
 
 def _per_scenario_errors(out, ref, cfg, k_sim, x0, ocfg):
@@ -37,7 +49,9 @@ def _per_scenario_errors(out, ref, cfg, k_sim, x0, ocfg):
     N = cfg.N
     g = {k: H(out[k]) for k in ("uk", "Uk", "xk", "wpred", "exitflag", "inner_iters")}
     div = np.where(((g["inner_iters"] != ref["inner_iters"]) | (g["exitflag"] != ref["exitflag"])).any(axis=0))[0]
-    assert len(div) <= 0.4 * x0.shape[1], len(div)
+    print(f"N={N} mode={cfg.mode}: {len(div)} of {x0.shape[1]} scenarios diverged in their iteration "
+          f"counts (replayed along the GPU's path): {[int(s) for s in div[:16]]}")
+    assert len(div) <= DIV_RECORDED[(N, cfg.mode)] + DIV_MARGIN, len(div)
     ref = {k: np.array(v, copy=True) for k, v in ref.items()}
     for s in div:
         rp = _replay_along(x0[:, s], ocfg, g["inner_iters"][:, s], None, int(s))
@@ -62,13 +76,16 @@ def test_run_closed_loop_wide(ctl, N, mode):
     out = ctl.run(T(x0), k_sim, cfg)
     d = np.load(GOLD / f"sensitivity_m{mode}_N{N}.npz")
     assert int(d["B"]) == B and int(d["k_sim"]) == k_sim
-    bound = np.maximum(RUN_TOL, SENS_FACTOR * d["sens"])
+    sens_bound = (N, mode) in SENS_BOUND
+    bound = np.maximum(RUN_TOL, SENS_FACTOR * d["sens"]) if sens_bound else np.full(B, RUN_TOL)
     e = _per_scenario_errors(out, ref, cfg, k_sim, x0, ocfg)
     wide = np.where(bound > RUN_TOL)[0]
+    above = int((e > RUN_TOL).sum())
     print(f"N={N} mode={mode}: max err {e.max():.2e} (scenario {int(np.argmax(e))}); {len(wide)} scenarios "
           f"bounded by {SENS_FACTOR:g} x the loop's sensitivity, max err / sens there "
           f"{np.max(e[wide] / d['sens'][wide], initial=0.0):.2f}")
-    print(f"   scenarios above RUN_TOL: {int((e > RUN_TOL).sum())}")
+    print(f"   scenarios above RUN_TOL: {above}")
+    assert above <= ABOVE_MAX.get((N, mode), 0), above
     bad = np.where(e > bound)[0]
     assert len(bad) == 0, [(int(s), float(e[s]), float(bound[s])) for s in bad]
 
