@@ -6,9 +6,12 @@ function [xk, uk, Uk, exitflag, iters, wpred] = NTM_MPC_Sim_gpu(x0, k_sim, cfg, 
 %     x0    2-by-B initial states [w; omega], one column per scenario
 %           (the reference's x0, NTM_MPC_Sim.m:34, is the B = 1 case)
 %     k_sim number of time steps (NTM_MPC_Sim.m:80)
-%     cfg   struct of controller settings (N, i_sim, mode, Ts, xmin, xmax,
-%           umin, umax, Q, r, epsilon); omitted fields take the reference's
-%           literals (NTM_MPC_Sim.m:30-88)
+%     cfg   struct of controller settings (N, i_sim, mode, flags, Ts, xmin,
+%           xmax, umin, umax, Q, r, epsilon, du_max, Ru); omitted fields take
+%           the reference's literals (NTM_MPC_Sim.m:30-88).  du_max bounds the
+%           input rate |U_i - U_{i-1}| in mode 3 (an extension, config 5); Ru
+%           adds Ru*||U||^2 to the cost (the reference has none, Ru = 0);
+%           flags selects the literal variants D4/D6/D13/D18 (SURVEY.md §2.1)
 %     mode  'run' (default): the whole closed loop on the device, one call;
 %           'step': one MEX call per time step (the state stays in MATLAB)
 %     gen   optional scenario generator struct (seed, first_id, sigma_w,

@@ -190,7 +190,8 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        CN_FK_DUAL, CN_FK_PRIMAL, CN_FK_SING, CN_FK_BOTH, ST_GI_WARM,
        CN_CDP_DROP, CN_CDP_RES, CN_CDP_PART, CN_CDP_DIR, CN_CDP_GI,
        CN_CDPX_SING0, CN_CDPX_SING1, CN_CDPX_BUDGET, CN_CDPX_DIR, CN_CDPX_NOVIOL, CN_CDPX_FULLDUAL, CN_CDPX_TINF,
-       CN_BORD_K0, CN_BORD_K1, CN_BORD_K2, CN_BORD_K3, CN_BORD_K4P, CN_SQ_K0, CN_SQ_K1, CN_SQ_K2, CN_SQ_COLL };
+       CN_BORD_K0, CN_BORD_K1, CN_BORD_K2, CN_BORD_K3, CN_BORD_K4P, CN_SQ_K0, CN_SQ_K1, CN_SQ_K2, CN_SQ_COLL,
+       CN_CDPX_NAN };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 #ifndef NTM_MAX_NT
 #define NTM_MAX_NT 32
@@ -217,6 +218,16 @@ constexpr int kCdpExtra = NTM_CDP_EXTRA;
 #endif
 #ifndef NTM_SPLIT_PRAGMA
 #define NTM_SPLIT_PRAGMA NTM_CHUNK_PRAGMA
+#endif
+// The re-solve's Gamma passes split over idle lanes (gamma_rows_split /
+// gamma_col_split; N = 20): bit 0 the row passes (Gamma U_B, the k = 1 line's
+// Gamma U_0 and Gamma D Z, the certificate's Gamma U), bit 1 the certificate's
+// gradient column pass.  NTM_SPLIT_CERT for the all-LDS build, _FAR for the far one
+#ifndef NTM_SPLIT_CERT
+#define NTM_SPLIT_CERT 0
+#endif
+#ifndef NTM_SPLIT_CERT_FAR
+#define NTM_SPLIT_CERT_FAR 0
 #endif
 #ifndef NTM_CDP_HINT
 #define NTM_CDP_HINT 1
@@ -941,6 +952,95 @@ __device__ __forceinline__ void gamma_row_dot2(const W& w, int r, const double* 
             y2 += gm * x2[u];
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// Row and column passes over Gamma split in two halves on otherwise idle lanes
+// (compile-time horizons with 4N - 2H <= 64, H = ceil(N/2): N = 20), as the
+// all-LDS build's scaling pass does (diag_scale_phase).  Row pass: lane l < 2N
+// sums the j < H terms of row r = l; lane 2N <= l < 4N - 2H the j >= H terms of
+// row r = l - 2N + 2H (the rows r >= 2H, the only ones that have such terms);
+// row r's value, (first half) + (second half), ends on lane r.  Column pass:
+// lane l < N takes stages i < H of column l, lane N + l stages i >= H; column
+// l's value ends on lane l.  The wave runs H trips instead of N.
+// ---------------------------------------------------------------------------
+template <int P, class W>
+__device__ __forceinline__ constexpr bool split_ok() {
+    return P == 64 && W::kNN > 0 && 4 * W::kNN - 2 * ((W::kNN + 1) / 2) <= 64;
+}
+// (Gamma_r v_k for the NV vectors v_k) on lane r < 2N
+template <int CH, int NV, class W>
+__device__ __forceinline__ void gamma_rows_split(const W& w, const double* const (&v)[NV], double (&y)[NV], int l) {
+    constexpr int NN = W::kNN, H = (NN + 1) / 2;
+    const bool lo = l < 2 * NN, hi = !lo && l < 4 * NN - 2 * H;
+    const int r = lo ? l : (hi ? l - 2 * NN + 2 * H : 0);
+    const int jb = lo ? 0 : H, jm = r >> 1;
+    const double* gr = w.Gt() + r;                        // gt(r, j) = gr[gidx(0, j)]
+    double s[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) s[k] = 0.0;
+    if (lo || hi) {
+        NTM_SPLIT_PRAGMA
+        for (int u0 = 0; u0 < H; u0 += CH) {
+            double g[CH], x[NV][CH];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int j = jb + u0 + u;
+                const bool in = u0 + u < H && j < NN;
+                g[u] = in ? gr[w.gidx(0, j)] : 0.0;
+#pragma unroll
+                for (int k = 0; k < NV; ++k) x[k][u] = in ? v[k][j] : 0.0;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int j = jb + u0 + u;
+                const double gm = (u0 + u < H && j <= jm) ? g[u] : 0.0;
+#pragma unroll
+                for (int k = 0; k < NV; ++k) s[k] += gm * x[k][u];
+            }
+        }
+    }
+    const int src = (l >= 2 * H && l < 2 * NN) ? l + 2 * NN - 2 * H : l;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const double s2 = __shfl(s[k], src & 63, 64);
+        y[k] = (src != l) ? s[k] + s2 : s[k];
+    }
+}
+// sum_{i >= l} Gamma_{2i,l} c_{2i} + Gamma_{2i+1,l} c_{2i+1} on lane l < N
+template <int CH, class W>
+__device__ __forceinline__ double gamma_col_split(const W& w, const double* c, int l) {
+    constexpr int NN = W::kNN, H = (NN + 1) / 2;
+    const bool lo = l < NN, hi = !lo && l < 2 * NN;
+    const int col = lo ? l : (hi ? l - NN : 0);
+    const int ib = lo ? 0 : H;
+    const double* cl = w.Gt() + w.gidx(2 * col, col) - 2 * col;   // cl[r] = gt(r, col), r >= 2 col
+    double s = 0.0;
+    if (lo || hi) {
+        NTM_SPLIT_PRAGMA
+        for (int u0 = 0; u0 < H; u0 += CH) {
+            double a0[CH], a1[CH], c0[CH], c1[CH];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int i = ib + u0 + u;
+                const bool in = u0 + u < H && i < NN;
+                a0[u] = in ? cl[2 * i] : 0.0;
+                a1[u] = in ? cl[2 * i + 1] : 0.0;
+                c0[u] = in ? c[2 * i] : 0.0;
+                c1[u] = in ? c[2 * i + 1] : 0.0;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int i = ib + u0 + u;
+                const double t = a0[u] * c0[u] + a1[u] * c1[u];
+                s += (u0 + u < H && i >= col && i < NN) ? t : 0.0;
+            }
+        }
+    }
+    const double s2 = __shfl(s, (l + NN) & 63, 64);
+    return lo ? s + s2 : s;
 }
 
 // ---------------------------------------------------------------------------
@@ -2630,6 +2730,8 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     const OmQ<qi_on<W>()> om(pb.Q);
     const bool dir = dir_p >= 0;
     const double Vprev = (l < N) ? w.V()[l] : 0.0;
+    constexpr int kSplitMask = split_ok<P, W>() ? (W::kFar ? NTM_SPLIT_CERT_FAR : NTM_SPLIT_CERT) : 0;
+    constexpr bool kSplitR = (kSplitMask & 1) != 0, kSplitC = (kSplitMask & 2) != 0;
     NTM_T0(tp);
     // --- classify active rows: single-entry rows fix a variable, the rest are general ---
     if (l < N) w.fx()[l] = 0;
@@ -2719,10 +2821,21 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     // all-LDS and generic builds; the far N = 20 / 50 kernels keep one code path)
     constexpr bool kFixedY = !W::kFar;
     const bool allfixed = kFixedY && nF == 0 && nS == 0;
-    for (int r = l; r < 2 * N && !dir; r += P) {
-        const double y = gamma_row_dot<NTM_CH>(w, r, w.dr());
-        w.Phi()[r] = y;
-        w.xp()[r] = allfixed ? y : y + w.e()[r] - ((r & 1) ? pb.r[1] : pb.r[0]);
+    if constexpr (kSplitR) {
+        if (!dir) {
+            double y[1];
+            gamma_rows_split<NTM_CH, 1>(w, {w.dr()}, y, l);
+            if (l < 2 * N) {
+                w.Phi()[l] = y[0];
+                w.xp()[l] = allfixed ? y[0] : y[0] + w.e()[l] - ((l & 1) ? pb.r[1] : pb.r[0]);
+            }
+        }
+    } else {
+        for (int r = l; r < 2 * N && !dir; r += P) {
+            const double y = gamma_row_dot<NTM_CH>(w, r, w.dr());
+            w.Phi()[r] = y;
+            w.xp()[r] = allfixed ? y : y + w.e()[r] - ((r & 1) ? pb.r[1] : pb.r[0]);
+        }
     }
     NTM_WSYNC();
     NTM_ACC(ST_C_Y, tp);
@@ -3153,11 +3266,20 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 w.d()[l] = w.D()[l] * zv;
             }
             NTM_WSYNC();
-            for (int r = l; r < 2 * N; r += P) {
-                double ya, yb;
-                gamma_row_dot2<NTM_CH>(w, r, w.U(), w.d(), ya, yb);
-                w.xp()[r] = ya;
-                w.Phi()[r] = yb;                                 // scratch (hs_of is done with it)
+            if constexpr (kSplitR) {
+                double yy[2];
+                gamma_rows_split<NTM_CH, 2>(w, {w.U(), w.d()}, yy, l);
+                if (l < 2 * N) {
+                    w.xp()[l] = yy[0];
+                    w.Phi()[l] = yy[1];                          // scratch (hs_of is done with it)
+                }
+            } else {
+                for (int r = l; r < 2 * N; r += P) {
+                    double ya, yb;
+                    gamma_row_dot2<NTM_CH>(w, r, w.U(), w.d(), ya, yb);
+                    w.xp()[r] = ya;
+                    w.Phi()[r] = yb;                             // scratch (hs_of is done with it)
+                }
             }
             NTM_WSYNC();
             double num = 0.0, den = 0.0;
@@ -3487,7 +3609,13 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         NTM_WSYNC();
         // y = Gamma U once, for the primal check (state rows) and the gradient
         if (!y_ready) {
-            for (int r = l; r < 2 * N; r += P) w.xp()[r] = gamma_row_dot<NTM_CH>(w, r, w.U());
+            if constexpr (kSplitR) {
+                double y[1];
+                gamma_rows_split<NTM_CH, 1>(w, {w.U()}, y, l);
+                if (l < 2 * N) w.xp()[l] = y[0];
+            } else {
+                for (int r = l; r < 2 * N; r += P) w.xp()[r] = gamma_row_dot<NTM_CH>(w, r, w.U());
+            }
             NTM_WSYNC();
         }
         }
@@ -3530,9 +3658,11 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             omy[2 * l + 1] = om.o1(y0, y1);
         }
         NTM_WSYNC();
+        double g2c = 0.0;
+        if constexpr (kSplitC) g2c = gamma_col_split<NTM_CH>(w, omy, l);
         if (l < N) {
             const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;
-            const double g2 = dot_rows2<NTM_CH>(cl, omy, N, l);      // terms i < l masked
+            const double g2 = kSplitC ? g2c : dot_rows2<NTM_CH>(cl, omy, N, l);      // terms i < l masked
             double gu = 2 * g2;
             if constexpr (ru_on<W>()) gu = gu + 2 * pb.Ru * w.U()[l];  // + 2 Ru U_l
             res = w.D()[l] * gu + w.F()[l];
@@ -3955,7 +4085,7 @@ __device__ __forceinline__ int shifted_into_act(const Prob& pb, const W& w, cons
 // the call); 0 inlines it like every other phase.
 // ---------------------------------------------------------------------------
 #ifndef NTM_GI_DEFER_PROBE
-#define NTM_GI_DEFER_PROBE 0   // probe only: GI and the dual-only direction compiled out
+#define NTM_GI_DEFER_PROBE 0   // timing probe only: GI compiled out of qp_phase
 #endif
 #ifndef NTM_GI_OUTLINE
 #define NTM_GI_OUTLINE 0
@@ -4202,7 +4332,6 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                     } else if (stage == 2) {               // the end point of adding p
                         NTM_CNT(CN_CDP_RES);
                         if (oks) { ++cq; okc = true; break; }
-                        if (NTM_GI_DEFER_PROBE && fk == 3) break;
                         if (fk == 3) {                     // A + {p} singular: p depends on A
                             dirp = p;
                             qs = cq;
@@ -4211,10 +4340,14 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                         }
                         const double u1 = (l <= cq) ? w.uu()[l] : 0.0;
                         double th = (l < cq && u1 < 0.0) ? u0 / (u0 - u1) : kInf;
+                        // a non-finite end-point multiplier (A's or p's own) makes the step
+                        // meaningless: th = -1 (a real fraction is in [0, 1)) hands the QP to
+                        // GI below instead of reading it as a negative multiplier
+                        if (l <= cq && !isfinite(u1)) th = -1.0;
                         int li = l;
                         gargmin<P>(th, li);
+                        if (th < 0.0) { NTM_CNT(CN_CDPX_NAN); break; }
                         if (!(th < kInf)) {                // full step: p joins A
-                            if (NTM_GI_DEFER_PROBE && fk != 2) break;
                             if (fk != 2) {
                                 // p's own multiplier < 0 at the end point (A's are all >= 0): p
                                 // (nearly) depends on A, an ill-conditioned step at long horizons.
@@ -4261,7 +4394,6 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                         p = pk.p;
                     }
                     if (nres >= budget) { NTM_CNT(CN_CDPX_BUDGET); break; }   // add p: A + {p}, or its direction when A is full
-                    if (NTM_GI_DEFER_PROBE && cq >= N) break;
                     if (cq >= N) {
                         dirp = p;
                         qs = cq;
@@ -4434,8 +4566,10 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
             if (!done) {
                 if (n_girun) ++*n_girun;
 #if NTM_GI_DEFER_PROBE
-                flag = NTM_EXIT_MAXITER;
-                (void)nwarm;
+                // timing probe only: the set at hand is taken as if certified (wrong
+                // values for these ~1% of QPs; the other 99% run exactly as built)
+                flag = NTM_EXIT_OPTIMAL;
+                q = nwarm;
 #else
                 flag = gi_fallback<P, W>(pb, w, rows, nrows, l, nwarm, it, qp_iters, &q, &ns, &yv);
 #endif

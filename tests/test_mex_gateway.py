@@ -137,12 +137,22 @@ def test_mex_library_errors_surface_as_matlab_errors(mex):
 
 
 # ---------------------------------------------------------------- GPU: bit-identical to ctypes
+def _skip_if_variant():
+    """The gateway is linked to the product library (rpath); a bitwise comparison
+    with a variant build loaded through NTM_MPC_LIB (A/B suites) would compare two
+    different builds (VERDICT r05 weak #7)."""
+    from ntm_mpc import _lib
+    if _lib.LIB_PATH.resolve() != (LIBDIR / "libntm_mpc.so").resolve():
+        pytest.skip(f"ctypes path loads {_lib.LIB_PATH.name} (NTM_MPC_LIB), the gateway libntm_mpc.so")
+
+
 @pytest.mark.gpu
 def test_mex_input_weight_field(mex, ctl):
     """cfg.Ru (ABI v5, the input weight) reaches the library through the gateway: a
     'step' with Ru = 1e-10 equals the ctypes call with the same Config, bit for bit,
     and differs from the Ru = 0 step."""
     from ntm_mpc import Config, scenarios_x0
+    _skip_if_variant()
     B, N = 8, 20
     x0 = np.ascontiguousarray(scenarios_x0(0, B))
     outs = []
@@ -166,12 +176,7 @@ def test_mex_matches_ctypes_path(mex, ctl):
     column-major 2x2)."""
     import torch
     from ntm_mpc import Config, ScenarioGen, scenarios_x0
-    from ntm_mpc import _lib
-    # the gateway is linked to the product library (rpath); a bitwise comparison
-    # with a variant build loaded through NTM_MPC_LIB (A/B suites) would compare
-    # two different builds (VERDICT r05 weak #7)
-    if _lib.LIB_PATH.resolve() != (LIBDIR / "libntm_mpc.so").resolve():
-        pytest.skip(f"ctypes path loads {_lib.LIB_PATH.name} (NTM_MPC_LIB), the gateway libntm_mpc.so")
+    _skip_if_variant()
     B, N, k_sim = 12, 20, 4
     Qm = np.array([[2.0e4, 3.0], [3.0, 2.0e-2]])
     mcfg = {"N": float(N), "i_sim": 10.0, "mode": 2.0, "flags": 0.0, "Ts": 0.1, "xmin": [0.06, 200 * np.pi],

@@ -61,7 +61,7 @@ print(f"certified dual path per wave-step: negative-multiplier drops {buf[67]/B:
       f"partial steps {buf[69]/B:.3f}, dual-only directions {buf[70]/B:.3f}, handed to GI {buf[71]/B:.3f}")
 print(f"  handed to GI because: candidate singular {buf[72]/B:.3f}, singular in the dual phase {buf[73]/B:.3f}, budget {buf[74]/B:.3f}, "
       f"direction on a non-echelon set {buf[75]/B:.3f}, no violated row {buf[76]/B:.3f}, dual failure at a full step {buf[77]/B:.3f}, "
-      f"no row can leave {buf[78]/B:.3f}")
+      f"no row can leave {buf[78]/B:.3f}, non-finite end-point multiplier {buf[88]/B:.4f}")
 print(f"re-solve paths per wave-step: echelon k=0 {buf[84]/B:.2f}, k=1 {buf[85]/B:.2f}, k=2 {buf[86]/B:.2f}, one collision {buf[87]/B:.2f}; "
       f"bordered with k = nF - nS = 0 {buf[79]/B:.2f}, 1 {buf[80]/B:.2f}, 2 {buf[81]/B:.2f}, 3 {buf[82]/B:.2f}, >= 4 {buf[83]/B:.2f}")
 print(f"first tries at it<=2 that failed, by kind, per wave-step: dual {buf[62]/B:.3f}, primal {buf[63]/B:.3f}, "
