@@ -124,7 +124,7 @@ int ntm_ctx_step_layout(const ntm_ctx* ctx, int32_t N, int64_t B, int32_t* far);
  * horizon (0 = generic).  ntm_ctx_step_layout is this with the default config. */
 int ntm_ctx_step_layout_cfg(const ntm_ctx* ctx, const ntm_config* cfg, int64_t B, int32_t* far, int32_t* lanes,
                             int32_t* horizon_template);
-/* Diagnostic builds only: per-phase s_memtime cycle totals and counters (80 entries);
+/* Diagnostic builds only: per-phase s_memtime cycle totals and counters (104 entries);
  * NTM_E_UNSUPPORTED in production builds. */
 int ntm_debug_stamps(unsigned long long* out32, int reset);
 /* Launch shape the step/run kernels use for horizon N: lanes per scenario

@@ -156,7 +156,7 @@ __shared__ int ntm_trace_grp;   // group (of this one-wave block) that owns the 
 // Diagnostic build only (-DNTM_STAMPS): per-phase s_memtime cycle totals,
 // summed over waves into ntm_stamps[] (read with ntm_debug_stamps).  The
 // production library compiles every stamp away.
-#define NTM_NSTAMPS 96
+#define NTM_NSTAMPS 104
 #ifdef NTM_STAMPS
 extern __device__ unsigned long long ntm_stamps[NTM_NSTAMPS];
 __shared__ unsigned long long ntm_lds_stamps[NTM_NSTAMPS];   // per block (= per wave), flushed once
@@ -191,7 +191,8 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        CN_CDP_DROP, CN_CDP_RES, CN_CDP_PART, CN_CDP_DIR, CN_CDP_GI,
        CN_CDPX_SING0, CN_CDPX_SING1, CN_CDPX_BUDGET, CN_CDPX_DIR, CN_CDPX_NOVIOL, CN_CDPX_FULLDUAL, CN_CDPX_TINF,
        CN_BORD_K0, CN_BORD_K1, CN_BORD_K2, CN_BORD_K3, CN_BORD_K4P, CN_SQ_K0, CN_SQ_K1, CN_SQ_K2, CN_SQ_COLL,
-       CN_CDPX_NAN };
+       CN_CDPX_NAN, CN_NAN_BORD, CN_NAN_K0, CN_NAN_K1, CN_NAN_K2, CN_NAN_COLL, CN_NAN_COLL2, CN_NAN_PRIMFAIL,
+       CN_NAN_V };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 #ifndef NTM_MAX_NT
 #define NTM_MAX_NT 32
@@ -1333,6 +1334,9 @@ typedef double ntm_d4 __attribute__((ext_vector_type(4)));
 #endif
 #ifndef NTM_COLL2
 #define NTM_COLL2 1        // square sets with two collisions on the null-space path (long horizons, generic)
+#endif
+#ifndef NTM_COLL3
+#define NTM_COLL3 1        // k = 2 sets with one collision (three holes) on the null-space path (round 6)
 #endif
 #ifndef NTM_ROWE_ALL
 #define NTM_ROWE_ALL 0     // 1: the echelon re-solve builds E one sorted row per lane at every horizon
@@ -2854,6 +2858,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     int nc2 = -1;                                          // k = 1 with one collision: the second hole
     int xb = -1;                                           // one collision: the row left out of the triangle
     int xb2 = -1;                                          // two collisions (k = 0): the second row left out
+    int nc3 = -1;                                          // k = 2 with one collision: the third hole
     const int kdim = nF - nS;
     // Long horizons with rate rows (config 5) mostly give square sets with ONE
     // collision: two general rows (a rate row and a state row of the same stage)
@@ -2867,6 +2872,11 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     // is minimised over the plane (a 2 x 2 system) instead of the bordered elimination
     constexpr bool kPlane = kCollision && NTM_PLANE;
     constexpr bool kColl2 = kCollision && NTM_COLL2;
+    // k = 2 with one collision (round 6): three holes and one row left out; the row
+    // left out fixes one of the three spare directions, the cost is minimised over
+    // the plane that remains (config 5 mode 3: 0.44 such sets per MPC step took the
+    // bordered elimination)
+    constexpr bool kColl3 = kPlane && NTM_COLL3;
     if ((kdim == 1 || (kdim == 0 && nS > 0) || (kPlane && kdim == 2 && nS > 0)) && !collide) {
         const unsigned long long fm = bal >> (lane & ~(P - 1));   // bit j: variable j is free
         int lastf = -1;
@@ -2898,19 +2908,24 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 perm[l] = colrow[c];
             }
             NTM_WSYNC();
-        } else if (kCollision && kdim <= 1 && (int)__popcll(holes) == kdim + 1 && (__ballot(l < nS && lastf < 0) & gmask) == 0) {
+        } else if (kCollision && kdim <= (kColl3 ? 2 : 1) && (int)__popcll(holes) == kdim + 1 &&
+                   (__ballot(l < nS && lastf < 0) & gmask) == 0) {
             // one row does not own its last column (the column's owner is the last writer):
-            // k = 0 leaves one hole, k = 1 two (the triangle's spare column and the collision's)
+            // k = 0 leaves one hole, k = 1 two (the triangle's spare column and the collision's),
+            // k = 2 three
             const unsigned long long orph = __ballot(l < nS && colrow[lastf < 0 ? 0 : lastf] != l) & gmask;
             if ((int)__popcll(orph) == 1) {
                 sq = true;
                 const unsigned long long hg = holes >> (lane & ~(P - 1));
+                const unsigned long long hg2 = hg & (hg - 1ull);
                 nc = uni<P>((int)__ffsll((long long)hg) - 1);
-                if (kdim == 1) nc2 = uni<P>((int)__ffsll((long long)(hg & (hg - 1ull))) - 1);
+                if (kdim >= 1) nc2 = uni<P>((int)__ffsll((long long)hg2) - 1);
+                if (kColl3 && kdim == 2) nc3 = uni<P>((int)__ffsll((long long)(hg2 & (hg2 - 1ull))) - 1);
                 xb = uni<P>((int)__ffsll((long long)(orph >> (lane & ~(P - 1)))) - 1);
                 if (l < nS - 1) {
                     int c = l + (l >= nc ? 1 : 0);
                     if (nc2 >= 0 && c >= nc2) ++c;
+                    if (kColl3 && nc3 >= 0 && c >= nc3) ++c;
                     perm[l] = colrow[c];
                 }
                 NTM_WSYNC();
@@ -3053,6 +3068,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         auto pc = [&](int u) {                                // pivot column of sorted row u
             int c = u + ((nc >= 0 && u >= nc) ? 1 : 0);
             if (kCollision && nc2 >= 0 && c >= nc2) ++c;
+            if (kColl3 && nc3 >= 0 && c >= nc3) ++c;
             return c;
         };
         double* const Ep = w.Ep();
@@ -3112,11 +3128,12 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             }
         }
         }
-        double acc = 0.0, acz = 0.0, acz2 = 0.0;
+        double acc = 0.0, acz = 0.0, acz2 = 0.0, acz3 = 0.0;
         if (l < n && !dir) {
             acc = hs_of(perm[l]);
             if (nc >= 0 && nc < pc(l)) acz = -gen_n(perm[l], w.fidx()[nc]);
             if (kCollision && nc2 >= 0 && nc2 < pc(l)) acz2 = -gen_n(perm[l], w.fidx()[nc2]);
+            if (kColl3 && nc3 >= 0 && nc3 < pc(l)) acz3 = -gen_n(perm[l], w.fidx()[nc3]);
         }
         const double hxb = (kCollision && xb >= 0 && !dir) ? hs_of(xb) : 0.0;   // before w.Phi() is reused
         const double hxb2 = (kColl2 && xb2 >= 0 && !dir) ? hs_of(xb2) : 0.0;
@@ -3126,7 +3143,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         if (!dir) {
         // E_p V_p = h and (k = 1) E_p Z_p = -e_c: lane t owns row t; step t broadcasts
         // x_t (z_t) and updates the rows below
-        double x = 0.0, zz = 0.0, zz2 = 0.0;
+        double x = 0.0, zz = 0.0, zz2 = 0.0, zz3 = 0.0;
         double en = (l > 0 && l < n) ? Ep[w.eidx(l, 0)] : 0.0;   // E[l][t], loaded one step ahead
         for (int t = 0; t < n; ++t) {
             const double et = en;
@@ -3144,12 +3161,18 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 if (l == t) zz2 = zt2;
                 acz2 -= et * zt2;
             }
+            if (kColl3 && nc3 >= 0) {
+                const double zt3 = gbcast<P>(acz3 * sq_id, t);
+                if (l == t) zz3 = zt3;
+                acz3 -= et * zt3;
+            }
         }
-        ok = gmaxi<P>((l < n && !(isfinite(x) && isfinite(zz) && isfinite(zz2))) ? 1 : 0) == 0;
+        ok = gmaxi<P>((l < n && !(isfinite(x) && isfinite(zz) && isfinite(zz2) && isfinite(zz3))) ? 1 : 0) == 0;
         // V_0 (pivots from E_p V_p = h, fixed values, 0 on the non-pivot columns) and Z
-        const bool hole = fpos == nc || (kCollision && nc2 >= 0 && fpos == nc2);
+        const bool hole = fpos == nc || (kCollision && nc2 >= 0 && fpos == nc2) || (kColl3 && nc3 >= 0 && fpos == nc3);
         const int rk = hole ? 0
-                            : fpos - ((nc >= 0 && fpos > nc) ? 1 : 0) - ((kCollision && nc2 >= 0 && fpos > nc2) ? 1 : 0);
+                            : fpos - ((nc >= 0 && fpos > nc) ? 1 : 0) - ((kCollision && nc2 >= 0 && fpos > nc2) ? 1 : 0) -
+                                  ((kColl3 && nc3 >= 0 && fpos > nc3) ? 1 : 0);
         const double xs = __shfl(x, (l < N && !fixed) ? rk : 0, P);
         const double zs = __shfl(zz, (l < N && !fixed) ? rk : 0, P);
         const double v0 = fixed ? vb : (hole ? 0.0 : xs);
@@ -3159,51 +3182,10 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         // V_p + w Z_d (eliminating the w with the larger |ai|) for the cost to minimise below
         double vline = v0, zline = 0.0;
         bool line = false;
-        if (kColl2 && ok && xb2 >= 0) {
-            // two collisions: V = V_0 + w1 Z1 + w2 Z2 with the rows left out fixing
-            // [n_B1'Z1 n_B1'Z2; n_B2'Z1 n_B2'Z2] w = [h_B1 - n_B1'V_0; h_B2 - n_B2'V_0]
-            const double zs2 = __shfl(zz2, (l < N && !fixed) ? rk : 0, P);
-            const double z1 = fixed ? 0.0 : ((fpos == nc) ? 1.0 : (hole ? 0.0 : zs));
-            const double z2 = fixed ? 0.0 : ((fpos == nc2) ? 1.0 : (hole ? 0.0 : zs2));
-            const double nb1 = (l < N && !fixed) ? gen_n(xb, l) : 0.0;
-            const double nb2 = (l < N && !fixed) ? gen_n(xb2, l) : 0.0;
-            const double b10 = gsum<P>(nb1 * v0), a11 = gsum<P>(nb1 * z1), a12 = gsum<P>(nb1 * z2);
-            const double b20 = gsum<P>(nb2 * v0), a21 = gsum<P>(nb2 * z1), a22 = gsum<P>(nb2 * z2);
-            const double det = a11 * a22 - a12 * a21;
-            const double scl = fmax(fmax(fabs(a11), fabs(a12)), fmax(fabs(a21), fabs(a22)));
-            ok = isfinite(det) && fabs(det) > 1e-14 * scl * scl && isfinite(b10) && isfinite(b20);
-            const double r1 = hxb - b10, r2 = hxb2 - b20;
-            const double w1 = ok ? (a22 * r1 - a12 * r2) / det : 0.0;
-            const double w2 = ok ? (a11 * r2 - a21 * r1) / det : 0.0;
-            vfin = v0 + w1 * z1 + w2 * z2;
-        } else if (kCollision && ok && xb >= 0 && nc2 >= 0) {
-            const double zs2 = __shfl(zz2, (l < N && !fixed) ? rk : 0, P);
-            const double z1 = fixed ? 0.0 : ((fpos == nc) ? 1.0 : (hole ? 0.0 : zs));
-            const double z2 = fixed ? 0.0 : ((fpos == nc2) ? 1.0 : (hole ? 0.0 : zs2));
-            const double nb = (l < N && !fixed) ? gen_n(xb, l) : 0.0;
-            const double b0 = gsum<P>(nb * v0), a1 = gsum<P>(nb * z1), a2 = gsum<P>(nb * z2);
-            const bool use2 = fabs(a2) >= fabs(a1);
-            const double ap = use2 ? a2 : a1, ao = use2 ? a1 : a2;
-            ok = ap != 0.0 && isfinite(ap) && isfinite(ao) && isfinite(b0);
-            const double zp = use2 ? z2 : z1, zo = use2 ? z1 : z2;
-            vline = ok ? v0 + ((hxb - b0) / ap) * zp : v0;
-            zline = ok ? zo - (ao / ap) * zp : 0.0;
-            line = ok;
-        } else if (kCollision && ok && xb >= 0) {
-            // the row left out fixes the step along Z: n_B' (V_0 + w Z) = h_B
-            const double zv = fixed ? 0.0 : ((fpos == nc) ? 1.0 : zs);
-            const double nb = (l < N && !fixed) ? gen_n(xb, l) : 0.0;
-            const double b0 = gsum<P>(nb * v0), b1 = gsum<P>(nb * zv);
-            ok = b1 != 0.0 && isfinite(b1) && isfinite(b0);
-            const double wv = ok ? (hxb - b0) / b1 : 0.0;
-            vfin = v0 + wv * zv;
-        } else if (kPlane && ok && nc2 >= 0) {
-            // k = 2: V = V_0 + w1 Z1 + w2 Z2 (Zi = e_{hole i} + Zi_p); with yi = Gamma D Zi
-            // and q = y_0 + e - r the cost is minimised at H w = -g, H_ij = yi' Om yj (+ Ru
-            // dUi' dUj), g_i = yi' Om q (+ Ru dUi' U_0): three Gamma passes, five reductions
-            const double zs2 = __shfl(zz2, (l < N && !fixed) ? rk : 0, P);
-            const double z1 = fixed ? 0.0 : ((fpos == nc) ? 1.0 : (hole ? 0.0 : zs));
-            const double z2 = fixed ? 0.0 : ((fpos == nc2) ? 1.0 : (hole ? 0.0 : zs2));
+        // k = 2: V = V_0 + w1 Z1 + w2 Z2 (Zi = e_{hole i} + Zi_p); with yi = Gamma D Zi
+        // and q = y_0 + e - r the cost is minimised at H w = -g, H_ij = yi' Om yj (+ Ru
+        // dUi' dUj), g_i = yi' Om q (+ Ru dUi' U_0): three Gamma passes, five reductions
+        auto plane_min = [&](const double v0, const double z1, const double z2) {
             double* const y2s = w.Vb();                       // 2N scratch (Vb, Uf: dead after hs_of)
             if (l < N) {
                 w.U()[l] = w.D()[l] * v0;
@@ -3253,6 +3235,68 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             vfin = v0 + w1 * z1 + w2 * z2;
             for (int r = l; r < 2 * N; r += P) w.xp()[r] += w1 * w.Phi()[r] + w2 * y2s[r];   // y
             y_ready = true;
+        };
+        if (kColl3 && ok && xb >= 0 && nc3 >= 0) {
+            // k = 2 with one collision: V = V_0 + w1 Z1 + w2 Z2 + w3 Z3; the row left out
+            // fixes a1 w1 + a2 w2 + a3 w3 = h_B - n_B' V_0 (ai = n_B' Zi): eliminating the w
+            // with the largest |ai| leaves the plane V_p + wa Za + wb Zb for the cost below
+            const double zs2 = __shfl(zz2, (l < N && !fixed) ? rk : 0, P);
+            const double zs3 = __shfl(zz3, (l < N && !fixed) ? rk : 0, P);
+            const double z1 = fixed ? 0.0 : ((fpos == nc) ? 1.0 : (hole ? 0.0 : zs));
+            const double z2 = fixed ? 0.0 : ((fpos == nc2) ? 1.0 : (hole ? 0.0 : zs2));
+            const double z3 = fixed ? 0.0 : ((fpos == nc3) ? 1.0 : (hole ? 0.0 : zs3));
+            const double nb = (l < N && !fixed) ? gen_n(xb, l) : 0.0;
+            const double b0 = gsum<P>(nb * v0), a1 = gsum<P>(nb * z1), a2 = gsum<P>(nb * z2), a3 = gsum<P>(nb * z3);
+            const int ip = (fabs(a3) > fabs(a2)) ? ((fabs(a3) > fabs(a1)) ? 3 : 1) : ((fabs(a2) >= fabs(a1)) ? 2 : 1);
+            const double ap = ip == 1 ? a1 : (ip == 2 ? a2 : a3);
+            const double aa = ip == 1 ? a2 : a1, ab = ip == 3 ? a2 : a3;
+            const double zp = ip == 1 ? z1 : (ip == 2 ? z2 : z3);
+            const double za = ip == 1 ? z2 : z1, zb = ip == 3 ? z2 : z3;
+            ok = ap != 0.0 && isfinite(ap) && isfinite(aa) && isfinite(ab) && isfinite(b0);
+            if (ok) plane_min(v0 + ((hxb - b0) / ap) * zp, za - (aa / ap) * zp, zb - (ab / ap) * zp);
+        } else if (kColl2 && ok && xb2 >= 0) {
+            // two collisions: V = V_0 + w1 Z1 + w2 Z2 with the rows left out fixing
+            // [n_B1'Z1 n_B1'Z2; n_B2'Z1 n_B2'Z2] w = [h_B1 - n_B1'V_0; h_B2 - n_B2'V_0]
+            const double zs2 = __shfl(zz2, (l < N && !fixed) ? rk : 0, P);
+            const double z1 = fixed ? 0.0 : ((fpos == nc) ? 1.0 : (hole ? 0.0 : zs));
+            const double z2 = fixed ? 0.0 : ((fpos == nc2) ? 1.0 : (hole ? 0.0 : zs2));
+            const double nb1 = (l < N && !fixed) ? gen_n(xb, l) : 0.0;
+            const double nb2 = (l < N && !fixed) ? gen_n(xb2, l) : 0.0;
+            const double b10 = gsum<P>(nb1 * v0), a11 = gsum<P>(nb1 * z1), a12 = gsum<P>(nb1 * z2);
+            const double b20 = gsum<P>(nb2 * v0), a21 = gsum<P>(nb2 * z1), a22 = gsum<P>(nb2 * z2);
+            const double det = a11 * a22 - a12 * a21;
+            const double scl = fmax(fmax(fabs(a11), fabs(a12)), fmax(fabs(a21), fabs(a22)));
+            ok = isfinite(det) && fabs(det) > 1e-14 * scl * scl && isfinite(b10) && isfinite(b20);
+            const double r1 = hxb - b10, r2 = hxb2 - b20;
+            const double w1 = ok ? (a22 * r1 - a12 * r2) / det : 0.0;
+            const double w2 = ok ? (a11 * r2 - a21 * r1) / det : 0.0;
+            vfin = v0 + w1 * z1 + w2 * z2;
+        } else if (kCollision && ok && xb >= 0 && nc2 >= 0) {
+            const double zs2 = __shfl(zz2, (l < N && !fixed) ? rk : 0, P);
+            const double z1 = fixed ? 0.0 : ((fpos == nc) ? 1.0 : (hole ? 0.0 : zs));
+            const double z2 = fixed ? 0.0 : ((fpos == nc2) ? 1.0 : (hole ? 0.0 : zs2));
+            const double nb = (l < N && !fixed) ? gen_n(xb, l) : 0.0;
+            const double b0 = gsum<P>(nb * v0), a1 = gsum<P>(nb * z1), a2 = gsum<P>(nb * z2);
+            const bool use2 = fabs(a2) >= fabs(a1);
+            const double ap = use2 ? a2 : a1, ao = use2 ? a1 : a2;
+            ok = ap != 0.0 && isfinite(ap) && isfinite(ao) && isfinite(b0);
+            const double zp = use2 ? z2 : z1, zo = use2 ? z1 : z2;
+            vline = ok ? v0 + ((hxb - b0) / ap) * zp : v0;
+            zline = ok ? zo - (ao / ap) * zp : 0.0;
+            line = ok;
+        } else if (kCollision && ok && xb >= 0) {
+            // the row left out fixes the step along Z: n_B' (V_0 + w Z) = h_B
+            const double zv = fixed ? 0.0 : ((fpos == nc) ? 1.0 : zs);
+            const double nb = (l < N && !fixed) ? gen_n(xb, l) : 0.0;
+            const double b0 = gsum<P>(nb * v0), b1 = gsum<P>(nb * zv);
+            ok = b1 != 0.0 && isfinite(b1) && isfinite(b0);
+            const double wv = ok ? (hxb - b0) / b1 : 0.0;
+            vfin = v0 + wv * zv;
+        } else if (kPlane && ok && nc2 >= 0) {
+            const double zs2 = __shfl(zz2, (l < N && !fixed) ? rk : 0, P);
+            const double z1 = fixed ? 0.0 : ((fpos == nc) ? 1.0 : (hole ? 0.0 : zs));
+            const double z2 = fixed ? 0.0 : ((fpos == nc2) ? 1.0 : (hole ? 0.0 : zs2));
+            plane_min(v0, z1, z2);
         } else if (ok && nc >= 0) {
             zline = fixed ? 0.0 : ((fpos == nc) ? 1.0 : zs);
             line = true;
@@ -3677,6 +3721,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             const int n = nS - (xb >= 0 ? 1 : 0) - (xb2 >= 0 ? 1 : 0);
             int pl = l + ((nc >= 0 && l >= nc) ? 1 : 0);             // lane t's pivot column
             if (kCollision && nc2 >= 0 && pl >= nc2) ++pl;
+            if (kColl3 && nc3 >= 0 && pl >= nc3) ++pl;
             double acc = (l < n) ? w.d()[pl] : 0.0, mu = 0.0;
             // one collision: a second right-hand side, the left-out row B at the pivot columns
             double acb = (kCollision && xb >= 0 && l < n) ? gen_n(xb, w.fidx()[pl]) : 0.0, mb = 0.0;
@@ -3723,6 +3768,12 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                     const double sa2 = gsum<P>(eh2 * mu), sb2 = gsum<P>(eh2 * mb);
                     const double den2 = gen_n(xb, w.fidx()[nc2]) - sb2;
                     if (fabs(den2) > fabs(den)) { den = den2; muB = (w.d()[nc2] - sa2) / den2; }
+                }
+                if (kColl3 && nc3 >= 0) {                  // k = 2: a third hole
+                    const double eh3 = (l < n && nc3 < pl) ? gen_n(perm[l], w.fidx()[nc3]) : 0.0;
+                    const double sa3 = gsum<P>(eh3 * mu), sb3 = gsum<P>(eh3 * mb);
+                    const double den3 = gen_n(xb, w.fidx()[nc3]) - sb3;
+                    if (fabs(den3) > fabs(den)) { den = den3; muB = (w.d()[nc3] - sa3) / den3; }
                 }
                 mu -= muB * mb;
                 if (l == 0) w.np()[xb] = muB;
@@ -3862,6 +3913,22 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             if (l < nS) mult_out[w.sidx()[l]] = w.np()[l];
             if (fixed) mult_out[w.fx()[l] - 1] = res / w.hv()[l];
         }
+#ifdef NTM_STAMPS
+        if (!dir) {                                        // non-finite multipliers, by re-solve path
+            const int nanm = gmaxi<P>(((l < nS && !isfinite(w.np()[l])) || (fixed && !isfinite(res / w.hv()[l]))) ? 1 : 0);
+            const int nanv = gmaxi<P>((l < N && !isfinite(vfin)) ? 1 : 0);
+            if (nanm) {
+                if (!sq) NTM_CNT(CN_NAN_BORD);
+                else if (xb2 >= 0) NTM_CNT(CN_NAN_COLL2);
+                else if (xb >= 0) NTM_CNT(CN_NAN_COLL);
+                else if (kdim == 0) NTM_CNT(CN_NAN_K0);
+                else if (kdim == 1) NTM_CNT(CN_NAN_K1);
+                else NTM_CNT(CN_NAN_K2);
+                if (!ok) NTM_CNT(CN_NAN_PRIMFAIL);
+                if (nanv) NTM_CNT(CN_NAN_V);
+            }
+        }
+#endif
         if (dir) {
             ok = gmaxi<P>(((l < nS && !isfinite(w.np()[l])) || (fixed && !isfinite(res / w.hv()[l]))) ? 1 : 0) == 0;
             fk = ok ? 0 : 3;

@@ -535,8 +535,11 @@ int launch_step(ntm_ctx* ctx, Prob pb, int64_t B, const double* x_k, double* rho
         if (!near)
             if (int rc = attach_far<NN>(ctx, pb, B, st)) return rc;
         const hipError_t e =
-            NN == 50 ? ntm_launch_step_n50(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, active_ws,
-                                           lds, st)
+            NN == 50 ? (pb.mode == NTM_MODE_FULL_DU
+                            ? ntm_launch_step_n50m3(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters,
+                                                    active_ws, lds, st)
+                            : ntm_launch_step_n50(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters,
+                                                  active_ws, lds, st))
             : near   ? ntm_launch_step_n20near(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters,
                                                active_ws, lds, st)
                      : ntm_launch_step_n20(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, active_ws,
@@ -579,7 +582,9 @@ int launch_run(ntm_ctx* ctx, Prob pb, int64_t B, int k_sim, const double* x0, do
         if (!near)
             if (int rc = attach_far<NN>(ctx, pb, B, st)) return rc;
         const hipError_t e =
-            NN == 50 ? ntm_launch_run_n50(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st)
+            NN == 50 ? (pb.mode == NTM_MODE_FULL_DU
+                            ? ntm_launch_run_n50m3(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st)
+                            : ntm_launch_run_n50(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st))
             : near   ? ntm_launch_run_n20near(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st)
                      : ntm_launch_run_n20(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st);
         const int rc = check_hip(ctx, e, "k_mpc_run<64,NN> launch");

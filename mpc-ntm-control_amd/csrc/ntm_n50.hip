@@ -16,6 +16,12 @@
 #endif
 #undef NTM_CH
 #define NTM_CH NTM_N50_CH
+// modes 0-2: without the three-hole null-space path, which only input-rate rows use
+// and which costs this kernel's register allocation 3.8% (config 5 mode 2: 76.6 vs
+// 79.5 ms, A/B on one box); mode 3 launches ntm_n50m3.hip
+#ifndef NTM_COLL3
+#define NTM_COLL3 0
+#endif
 #include "ntm_step.h"
 
 NTM_DEFINE_LAYOUT_LAUNCHERS(n50, 50, true)

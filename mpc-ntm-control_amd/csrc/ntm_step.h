@@ -289,7 +289,12 @@ __global__ __launch_bounds__(64, NTM_WAVES_PER_EU_P(P, NN, FAR)) void k_mpc_run(
 
 // Launchers of one horizon's one-wave-per-scenario kernels (grid of one 64-lane
 // block per scenario, lds bytes each), instantiated by the translation unit that
-// owns that horizon (ntm_n20.hip, ntm_n50.hip: each sets its own LDS batch size)
+// owns that horizon (ntm_n20.hip, ntm_n50.hip: each sets its own LDS batch size).
+// Internal linkage: two translation units that build the same horizon with
+// different settings (ntm_n50.hip and ntm_n50m3.hip) instantiate these templates
+// with the same arguments, and external (COMDAT) instances would be folded into
+// one of the two builds at link time
+namespace {
 template <typename K>
 hipError_t ntm_lds_opt_in(K kern, size_t lds) {
     if (lds <= 64 * 1024) return hipSuccess;
@@ -326,8 +331,10 @@ hipError_t ntm_launch_run_v(const ntm::Prob& pb, int64_t B, int k_sim, const dou
                        wpred, exitflag, inner_iters);
     return hipGetLastError();
 }
+}  // namespace
 // One translation unit per (horizon, layout): ntm_n20.hip (far), ntm_n20near.hip (the
-// all-LDS N = 20 build for small batches, its own batch settings), ntm_n50.hip (far)
+// all-LDS N = 20 build for small batches, its own batch settings), ntm_n50.hip (far,
+// modes 0-2) and ntm_n50m3.hip (far, input-rate rows: mode 3)
 #define NTM_DECLARE_LAYOUT_LAUNCHERS(NAME)                                                                         \
     hipError_t ntm_launch_step_##NAME(const ntm::Prob& pb, int64_t B, const double* x_k, double* rho,             \
                                       double* U_old, double* U, double* x_pred, double* x_next, int32_t* exitflag, \
@@ -350,3 +357,4 @@ hipError_t ntm_launch_run_v(const ntm::Prob& pb, int64_t B, int k_sim, const dou
 NTM_DECLARE_LAYOUT_LAUNCHERS(n20)
 NTM_DECLARE_LAYOUT_LAUNCHERS(n20near)
 NTM_DECLARE_LAYOUT_LAUNCHERS(n50)
+NTM_DECLARE_LAYOUT_LAUNCHERS(n50m3)

@@ -20,6 +20,7 @@ cp $G/pmc/sq_$T.json $P/sq_$T.json
 mkdir -p $P/${T}_configs $P/${T}_dist
 cp $G/cfg/c2.json $G/cfg/c5m2.json $G/cfg/c5m3.json $G/cfg/pcie.log $P/${T}_configs/
 cp $G/dist/w1_nccl.json $G/dist/w2_gloo.json $P/${T}_dist/
+[ -f $G/dist/w2_launcher.json ] && cp $G/dist/w2_launcher.json $P/${T}_dist/
 tail -3 $G/parity.log > $P/${T}_gpu_tests.txt
 cp $G/mfma_pmc/mfma_counter_collection.csv $P/${T}_pmc_mfma_n50.csv
 echo "copied into $P/ (${T})"

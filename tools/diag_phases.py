@@ -13,7 +13,7 @@ N = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 cfg = Config(N=N, mode=int(sys.argv[3]) if len(sys.argv) > 3 else 2)
 ctl = NtmMpc(config=cfg)
 lib = ntm_mpc.load()
-buf = (C.c_ulonglong * 96)()
+buf = (C.c_ulonglong * 104)()
 x = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(0, B))
 rho, uo = ctl.initial_state(x, cfg)
 ws = ctl.new_active_ws(B, cfg)
@@ -62,6 +62,9 @@ print(f"certified dual path per wave-step: negative-multiplier drops {buf[67]/B:
 print(f"  handed to GI because: candidate singular {buf[72]/B:.3f}, singular in the dual phase {buf[73]/B:.3f}, budget {buf[74]/B:.3f}, "
       f"direction on a non-echelon set {buf[75]/B:.3f}, no violated row {buf[76]/B:.3f}, dual failure at a full step {buf[77]/B:.3f}, "
       f"no row can leave {buf[78]/B:.3f}, non-finite end-point multiplier {buf[88]/B:.4f}")
+print(f"re-solves with non-finite multipliers per wave-step, by path: bordered {buf[89]/B:.4f}, echelon k=0 {buf[90]/B:.4f}, "
+      f"k=1 {buf[91]/B:.4f}, k=2 {buf[92]/B:.4f}, one collision {buf[93]/B:.4f}, two collisions {buf[94]/B:.4f}; "
+      f"of them primal check failed {buf[95]/B:.4f}, V non-finite {buf[96]/B:.4f}")
 print(f"re-solve paths per wave-step: echelon k=0 {buf[84]/B:.2f}, k=1 {buf[85]/B:.2f}, k=2 {buf[86]/B:.2f}, one collision {buf[87]/B:.2f}; "
       f"bordered with k = nF - nS = 0 {buf[79]/B:.2f}, 1 {buf[80]/B:.2f}, 2 {buf[81]/B:.2f}, 3 {buf[82]/B:.2f}, >= 4 {buf[83]/B:.2f}")
 print(f"first tries at it<=2 that failed, by kind, per wave-step: dual {buf[62]/B:.3f}, primal {buf[63]/B:.3f}, "

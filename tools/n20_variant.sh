@@ -10,5 +10,5 @@ H="/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unu
 mkdir -p lib/obj_$V
 SCHED=${SCHED:--mllvm -amdgpu-use-amdgpu-trackers=1}   # the product flags of ntm_n20.o (Makefile N20FLAGS)
 $H $SCHED $F -c -o lib/obj_$V/ntm_n20.o csrc/ntm_n20.hip
-$H -shared -o lib/libntm_mpc_$V.so lib/obj/ntm_kernels.o lib/obj_$V/ntm_n20.o lib/obj/ntm_n20near.o lib/obj/ntm_n50.o
+$H -shared -o lib/libntm_mpc_$V.so lib/obj/ntm_kernels.o lib/obj_$V/ntm_n20.o lib/obj/ntm_n20near.o lib/obj/ntm_n50.o lib/obj/ntm_n50m3.o
 echo built lib/libntm_mpc_$V.so

@@ -7,5 +7,5 @@ V=$1; F=$2
 H="/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function"
 mkdir -p lib/obj_$V
 $H $F -c -o lib/obj_$V/ntm_n20near.o csrc/ntm_n20near.hip
-$H -shared -o lib/libntm_mpc_$V.so lib/obj/ntm_kernels.o lib/obj/ntm_n20.o lib/obj_$V/ntm_n20near.o lib/obj/ntm_n50.o
+$H -shared -o lib/libntm_mpc_$V.so lib/obj/ntm_kernels.o lib/obj/ntm_n20.o lib/obj_$V/ntm_n20near.o lib/obj/ntm_n50.o lib/obj/ntm_n50m3.o
 echo built lib/libntm_mpc_$V.so
