@@ -326,6 +326,33 @@ def pdas(qp, cand, alt_set, budget=8, cap_add=None):
     return False, n
 
 
+def pdas_then_gi(qp, cand, k):
+    """k primal-dual exchanges (every violated row in, every negative multiplier out),
+    then the certified dual path from the last set (steered by the shifted set)."""
+    act, n = list(cand), 0
+    for rep in range(k):
+        fk, U, mu, s = qp.solve(act)
+        n += 1
+        if fk == 0:
+            return True, n
+        if fk == 3:
+            break
+        mtol = -1e-9 * max(1.0, np.abs(mu).max()) if len(act) else 0
+        keep = [a for k2, a in enumerate(act) if mu[k2] >= mtol]
+        sm = s.copy()
+        sm[act] = np.inf
+        viol = [int(i) for i in np.argsort(sm) if sm[i] < -1e-9 * max(1.0, np.abs(U / qp.D).max())]
+        for p in viol:
+            jl = int(qp.last[p]) if qp.kind(p) >= 2 else -1
+            if jl >= 0:
+                keep = [a for a in keep if not (qp.kind(a) < 2 and qp.last[a] == jl)]
+            if p not in keep:
+                keep.append(p)
+        act = keep[:N]
+    ok, n2 = gi_resolve(qp, act, None, 64, hint=HINTS.get("s10"))
+    return ok, n + n2
+
+
 x = O.scenario_x0(np.arange(S)).T.copy()
 rho, Uo = cbind.initial_state(x, cfg)
 for _ in range(lo - 2):
@@ -339,6 +366,11 @@ strategies = {
     "GI: hint shift(prev 2)": lambda q, c, a: gi_resolve(q, c, a, 64, hint=HINTS.get("s2")),
     "GI: hint shift(p10) + shift(p2)": lambda q, c, a: gi_resolve(q, c, a, 64, hint=HINTS.get("u")),
     "GI by re-solves (64)": lambda q, c, a: gi_resolve(q, c, a, 64),
+    # round 6: the odd plan's set change at this step (O_{k+1} vs O_k) carried to the even set
+    "GI: hint shift(p10) + odd delta": lambda q, c, a: gi_resolve(q, c, a, 64, hint=HINTS.get("sd")),
+    "GI: delta cand + hint shift(p10)": lambda q, c, a: gi_resolve(q, HINTS.get("dc", c), a, 64, hint=HINTS.get("s10")),
+    "PDAS (8)": lambda q, c, a: pdas(q, c, None, 8),
+    "PDAS (2) then GI path": lambda q, c, a: pdas_then_gi(q, c, 2),
 }
 res = {it: {k: [0, 0, 0] for k in strategies} for it in ITERS}   # certified, re-solves, count
 exact = {it: 0 for it in ITERS}
@@ -368,6 +400,13 @@ for s in range(S):
                 if it == 2 and 2 in prev:
                     HINTS.update(s10=shift(prev[10]), p2=list(prev[2]), s2=shift(prev[2]),
                                  u=list(dict.fromkeys(shift(prev[10]) + shift(prev[2]))))
+                    if 1 in sets and 9 in prev:
+                        add = [i for i in sets[1] if i not in prev[9]]
+                        drop = set(i for i in prev[9] if i not in sets[1])
+                        HINTS.update(sd=list(dict.fromkeys(add + shift(prev[10]))))
+                        dc = [i for i in cand if i not in drop] + [i for i in add if i not in cand]
+                        if len(dc) <= N:
+                            HINTS.update(dc=dc)
                 elif it == 1:
                     HINTS.update(s10=shift(prev[9]), p2=list(prev[10]), s2=list(prev[1]) if 1 in prev else None)
                 elif it >= 3 and it - 1 in sets:
