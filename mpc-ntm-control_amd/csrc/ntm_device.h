@@ -192,7 +192,7 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        CN_CDPX_SING0, CN_CDPX_SING1, CN_CDPX_BUDGET, CN_CDPX_DIR, CN_CDPX_NOVIOL, CN_CDPX_FULLDUAL, CN_CDPX_TINF,
        CN_BORD_K0, CN_BORD_K1, CN_BORD_K2, CN_BORD_K3, CN_BORD_K4P, CN_SQ_K0, CN_SQ_K1, CN_SQ_K2, CN_SQ_COLL,
        CN_CDPX_NAN, CN_NAN_BORD, CN_NAN_K0, CN_NAN_K1, CN_NAN_K2, CN_NAN_COLL, CN_NAN_COLL2, CN_NAN_PRIMFAIL,
-       CN_NAN_V };
+       CN_NAN_V, CN_BX_O1, CN_BX_O2, CN_BX_O3P, CN_BX_NEG, CN_BX_NOCLASS };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 #ifndef NTM_MAX_NT
 #define NTM_MAX_NT 32
@@ -2860,6 +2860,14 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     int xb2 = -1;                                          // two collisions (k = 0): the second row left out
     int nc3 = -1;                                          // k = 2 with one collision: the third hole
     const int kdim = nF - nS;
+#ifdef NTM_STAMPS
+    int dg_orph = -1, dg_neg = 0;                          // diagnostic: the shape of a set left to the bordered path
+#endif
+    // a general row with no non-zero at a free column makes the KKT matrix singular
+    // (its row of E is zero): rejected like a colliding set (fail kind 3) instead of
+    // running the bordered elimination into a zero pivot (long horizons: N = 50 mode 2
+    // met 0.11 such re-solves per MPC step, round 6)
+    bool nofree = false;
     // Long horizons with rate rows (config 5) mostly give square sets with ONE
     // collision: two general rows (a rate row and a state row of the same stage)
     // end in the same free column, and one column has no row ending there (83% of
@@ -2897,6 +2905,11 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         if (lastf >= 0) colrow[lastf] = l;                     // a repeated last column leaves a hole
         NTM_WSYNC();
         const unsigned long long holes = __ballot(l < nF && colrow[l] < 0) & gmask;
+        if constexpr (kCollision) nofree = (__ballot(l < nS && lastf < 0) & gmask) != 0;
+#ifdef NTM_STAMPS
+        dg_neg = (__ballot(l < nS && lastf < 0) & gmask) != 0;
+        dg_orph = (int)__popcll(__ballot(l < nS && lastf >= 0 && colrow[lastf] != l) & gmask);
+#endif
         if ((int)__popcll(holes) == kdim) {                    // every row ends in its own column
             sq = true;
             const unsigned long long hg = holes >> (lane & ~(P - 1));
@@ -2930,22 +2943,27 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 }
                 NTM_WSYNC();
             }
-        } else if (kColl2 && kdim == 0 && (int)__popcll(holes) == 2 && (__ballot(l < nS && lastf < 0) & gmask) == 0) {
+        } else if (kColl2 && kdim <= (kColl3 ? 1 : 0) && (int)__popcll(holes) == kdim + 2 &&
+                   (__ballot(l < nS && lastf < 0) & gmask) == 0) {
             // two rows do not own their last columns (square set, two holes): leaving both
             // out leaves an echelon system with two spare columns, and the two rows left out
-            // fix the step along the plane instead of the cost (round 5, rate rows at N = 50)
+            // fix the step along the plane instead of the cost (round 5, rate rows at N = 50);
+            // k = 1 leaves three holes, and the two rows fix a line (round 6, NTM_COLL3)
             const unsigned long long orph = __ballot(l < nS && colrow[lastf < 0 ? 0 : lastf] != l) & gmask;
             if ((int)__popcll(orph) == 2) {
                 sq = true;
                 const unsigned long long hg = holes >> (lane & ~(P - 1));
+                const unsigned long long hg2 = hg & (hg - 1ull);
                 nc = uni<P>((int)__ffsll((long long)hg) - 1);
-                nc2 = uni<P>((int)__ffsll((long long)(hg & (hg - 1ull))) - 1);
+                nc2 = uni<P>((int)__ffsll((long long)hg2) - 1);
+                if (kColl3 && kdim == 1) nc3 = uni<P>((int)__ffsll((long long)(hg2 & (hg2 - 1ull))) - 1);
                 const unsigned long long og = orph >> (lane & ~(P - 1));
                 xb = uni<P>((int)__ffsll((long long)og) - 1);
                 xb2 = uni<P>((int)__ffsll((long long)(og & (og - 1ull))) - 1);
                 if (l < nS - 2) {
                     int c = l + (l >= nc ? 1 : 0);
                     if (c >= nc2) ++c;
+                    if (kColl3 && nc3 >= 0 && c >= nc3) ++c;
                     perm[l] = colrow[c];
                 }
                 NTM_WSYNC();
@@ -2969,6 +2987,13 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         else if (kdim == 2) NTM_CNT(CN_BORD_K2);
         else if (kdim == 3) NTM_CNT(CN_BORD_K3);
         else NTM_CNT(CN_BORD_K4P);
+        if (!sq) {
+            if (dg_orph < 0) NTM_CNT(CN_BX_NOCLASS);
+            else if (dg_neg) NTM_CNT(CN_BX_NEG);
+            else if (dg_orph == 1) NTM_CNT(CN_BX_O1);
+            else if (dg_orph == 2) NTM_CNT(CN_BX_O2);
+            else if (dg_orph >= 3) NTM_CNT(CN_BX_O3P);
+        }
     }
 #endif
     // --- g_F (lane a = compact index) ---
@@ -3055,7 +3080,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         return hs;
     };
     NTM_ACC(ST_P_GRAM, tp);
-    bool ok = !collide;
+    bool ok = !collide && !nofree;
     int fk = ok ? 0 : 3, fpos_out = 0;
     double vfin = 0.0;
     double sq_id = 0.0;                                   // echelon path: 1 / E_p[t][t] on lane t
@@ -3236,7 +3261,36 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             for (int r = l; r < 2 * N; r += P) w.xp()[r] += w1 * w.Phi()[r] + w2 * y2s[r];   // y
             y_ready = true;
         };
-        if (kColl3 && ok && xb >= 0 && nc3 >= 0) {
+        if (kColl3 && ok && xb2 >= 0 && nc3 >= 0) {
+            // k = 1 with two collisions: V = V_0 + w1 Z1 + w2 Z2 + w3 Z3 and the two rows left
+            // out fix A w = r (A 2 x 3, A_ij = n_Bi' Zj, r_i = h_Bi - n_Bi' V_0): a particular
+            // solution from the best-conditioned 2 x 2 minor plus t times the null vector
+            // (the rows' cross product) leaves the line V_p + t Z_n for the cost to minimise
+            const double zs2 = __shfl(zz2, (l < N && !fixed) ? rk : 0, P);
+            const double zs3 = __shfl(zz3, (l < N && !fixed) ? rk : 0, P);
+            const double z1 = fixed ? 0.0 : ((fpos == nc) ? 1.0 : (hole ? 0.0 : zs));
+            const double z2 = fixed ? 0.0 : ((fpos == nc2) ? 1.0 : (hole ? 0.0 : zs2));
+            const double z3 = fixed ? 0.0 : ((fpos == nc3) ? 1.0 : (hole ? 0.0 : zs3));
+            const double nb1 = (l < N && !fixed) ? gen_n(xb, l) : 0.0;
+            const double nb2 = (l < N && !fixed) ? gen_n(xb2, l) : 0.0;
+            const double b10 = gsum<P>(nb1 * v0), a11 = gsum<P>(nb1 * z1), a12 = gsum<P>(nb1 * z2), a13 = gsum<P>(nb1 * z3);
+            const double b20 = gsum<P>(nb2 * v0), a21 = gsum<P>(nb2 * z1), a22 = gsum<P>(nb2 * z2), a23 = gsum<P>(nb2 * z3);
+            const double r1 = hxb - b10, r2 = hxb2 - b20;
+            const double d12 = a11 * a22 - a12 * a21, d13 = a11 * a23 - a13 * a21, d23 = a12 * a23 - a13 * a22;
+            const double scl = fmax(fmax(fmax(fabs(a11), fabs(a12)), fabs(a13)), fmax(fmax(fabs(a21), fabs(a22)), fabs(a23)));
+            const int im = (fabs(d12) >= fabs(d13) && fabs(d12) >= fabs(d23)) ? 0 : (fabs(d13) >= fabs(d23) ? 1 : 2);
+            const double dm = im == 0 ? d12 : (im == 1 ? d13 : d23);
+            ok = isfinite(dm) && fabs(dm) > 1e-14 * scl * scl && isfinite(b10) && isfinite(b20);
+            double w1 = 0.0, w2 = 0.0, w3 = 0.0;
+            if (ok) {
+                if (im == 0) { w1 = (a22 * r1 - a12 * r2) / dm; w2 = (a11 * r2 - a21 * r1) / dm; }
+                else if (im == 1) { w1 = (a23 * r1 - a13 * r2) / dm; w3 = (a11 * r2 - a21 * r1) / dm; }
+                else { w2 = (a23 * r1 - a13 * r2) / dm; w3 = (a12 * r2 - a22 * r1) / dm; }
+            }
+            vline = ok ? v0 + w1 * z1 + w2 * z2 + w3 * z3 : v0;
+            zline = ok ? (d23 / dm) * z1 - (d13 / dm) * z2 + (d12 / dm) * z3 : 0.0;
+            line = ok;
+        } else if (kColl3 && ok && xb >= 0 && nc3 >= 0) {
             // k = 2 with one collision: V = V_0 + w1 Z1 + w2 Z2 + w3 Z3; the row left out
             // fixes a1 w1 + a2 w2 + a3 w3 = h_B - n_B' V_0 (ai = n_B' Zi): eliminating the w
             // with the largest |ai| leaves the plane V_p + wa Za + wb Zb for the cost below
@@ -3749,10 +3803,23 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 const double e2 = (l < n && nc2 < pl) ? gen_n(perm[l], w.fidx()[nc2]) : 0.0;
                 const double sa1 = gsum<P>(e1 * mu), s11 = gsum<P>(e1 * mb), s12 = gsum<P>(e1 * mb2);
                 const double sa2 = gsum<P>(e2 * mu), s21 = gsum<P>(e2 * mb), s22 = gsum<P>(e2 * mb2);
-                const double m11 = gen_n(xb, w.fidx()[nc]) - s11, m12 = gen_n(xb2, w.fidx()[nc]) - s12;
-                const double m21 = gen_n(xb, w.fidx()[nc2]) - s21, m22 = gen_n(xb2, w.fidx()[nc2]) - s22;
-                const double q1 = w.d()[nc] - sa1, q2 = w.d()[nc2] - sa2;
-                const double det = m11 * m22 - m12 * m21;
+                double m11 = gen_n(xb, w.fidx()[nc]) - s11, m12 = gen_n(xb2, w.fidx()[nc]) - s12;
+                double m21 = gen_n(xb, w.fidx()[nc2]) - s21, m22 = gen_n(xb2, w.fidx()[nc2]) - s22;
+                double q1 = w.d()[nc] - sa1, q2 = w.d()[nc2] - sa2;
+                double det = m11 * m22 - m12 * m21;
+                if (kColl3 && nc3 >= 0) {
+                    // k = 1: three hole equations, two unknowns; the best-conditioned pair
+                    const double e3 = (l < n && nc3 < pl) ? gen_n(perm[l], w.fidx()[nc3]) : 0.0;
+                    const double sa3 = gsum<P>(e3 * mu), s31 = gsum<P>(e3 * mb), s32 = gsum<P>(e3 * mb2);
+                    const double m31 = gen_n(xb, w.fidx()[nc3]) - s31, m32 = gen_n(xb2, w.fidx()[nc3]) - s32;
+                    const double q3 = w.d()[nc3] - sa3;
+                    const double det13 = m11 * m32 - m12 * m31, det23 = m21 * m32 - m22 * m31;
+                    if (fabs(det13) > fabs(det) && fabs(det13) >= fabs(det23)) {
+                        m21 = m31; m22 = m32; q2 = q3; det = det13;
+                    } else if (fabs(det23) > fabs(det)) {
+                        m11 = m31; m12 = m32; q1 = q3; det = -det23;   // rows (3, 2): det = m31 m22 - m32 m21
+                    }
+                }
                 const double mu1 = (m22 * q1 - m12 * q2) / det, mu2 = (m11 * q2 - m21 * q1) / det;
                 mu -= mu1 * mb + mu2 * mb2;
                 if (l == 0) { w.np()[xb] = mu1; w.np()[xb2] = mu2; }
