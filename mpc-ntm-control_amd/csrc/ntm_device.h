@@ -192,7 +192,7 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        CN_CDPX_SING0, CN_CDPX_SING1, CN_CDPX_BUDGET, CN_CDPX_DIR, CN_CDPX_NOVIOL, CN_CDPX_FULLDUAL, CN_CDPX_TINF,
        CN_BORD_K0, CN_BORD_K1, CN_BORD_K2, CN_BORD_K3, CN_BORD_K4P, CN_SQ_K0, CN_SQ_K1, CN_SQ_K2, CN_SQ_COLL,
        CN_CDPX_NAN, CN_NAN_BORD, CN_NAN_K0, CN_NAN_K1, CN_NAN_K2, CN_NAN_COLL, CN_NAN_COLL2, CN_NAN_PRIMFAIL,
-       CN_NAN_V, CN_BX_O1, CN_BX_O2, CN_BX_O3P, CN_BX_NEG, CN_BX_NOCLASS };
+       CN_NAN_V, CN_BX_O1, CN_BX_O2, CN_BX_O3P, CN_BX_NEG, CN_BX_NOCLASS, CN_CDP_SKIP };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 #ifndef NTM_MAX_NT
 #define NTM_MAX_NT 32
@@ -229,6 +229,10 @@ constexpr int kCdpExtra = NTM_CDP_EXTRA;
 #endif
 #ifndef NTM_SPLIT_CERT_FAR
 #define NTM_SPLIT_CERT_FAR 0
+#endif
+// the dual path's skip of a row whose A + {p} end point is non-finite (long horizons)
+#ifndef NTM_CDP_SKIP
+#define NTM_CDP_SKIP 1
 #endif
 #ifndef NTM_CDP_HINT
 #define NTM_CDP_HINT 1
@@ -1761,6 +1765,7 @@ struct Pick {
 // aflag bits per constraint row
 constexpr unsigned char kActiveRow = 1;   // in GI's active set
 constexpr unsigned char kCandRow = 2;     // row of a failed warm-start candidate (GI adds these first)
+constexpr unsigned char kSkipRow = 4;     // dual path (long horizons): p left out until the active set changes
 
 // Implicit getWLc rows: u-bounds are -+e_j, state rows are -+Gamma_r; the
 // rows are never materialised.
@@ -1883,7 +1888,8 @@ struct StructRows {
         auto consider = [&](double s, int id, double bcv) {
             if (verify) { bad |= s < -1e-9 * fmax(vmax, fabs(bcv)); return; }
             const unsigned char fl = w.aflag()[id];
-            if (fl & kActiveRow) return;
+            constexpr unsigned char kOut = (W::kNN > 32 || W::kNN == 0) ? (kActiveRow | kSkipRow) : kActiveRow;
+            if (fl & kOut) return;
             const double key = ((fl & kCandRow) && s < -1e-12 * fmax(vmax, fabs(bcv))) ? s - 1e200 : s;
             if (key < bv || (key == bv && id < bid)) { bv = key; bid = id; bs = s; bbc = bcv; }
         };
@@ -4363,6 +4369,21 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                 // dual-only direction of row dirp on A.  stage 0: the carried set;
                 // 1: dropping negative multipliers; 2: A + {p}; 3: the direction of p
                 int stage = 0, qs = cq, dirp = -1, p = -1, nres = 0, fk = 0, fp = 0;
+                // Long horizons: an A + {p} whose end point has a non-finite multiplier (p
+                // (nearly) depends on A) leaves p out (kSkipRow) and adds another violated row
+                // instead, as the dual method may add any violated row; p is eligible again
+                // once A changes.  Before round 6 these QPs went to GI (N = 50 mode 2: 0.1 per
+                // MPC step, 7% of the cycles)
+                constexpr bool kSkipNan = NTM_CDP_SKIP && (W::kNN > 32 || W::kNN == 0);
+                int nskip = 0;
+                bool fresh_y = false;                      // the pick recomputes y = Gamma U at V0
+                auto clear_skips = [&]() {
+                    if (kSkipNan && nskip > 0) {
+                        for (int i = l; i < nrows; i += P) w.aflag()[i] &= (unsigned char)~kSkipRow;
+                        NTM_WSYNC();
+                        nskip = 0;
+                    }
+                };
                 // iteration 2 at N <= 32 starts from the unshifted carried set; the dual
                 // path then adds violated rows of its receding-horizon shift first
                 // (StructRows::check prefers kCandRow rows).  Offline (tools/repair_study.py,
@@ -4480,8 +4501,17 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                         if (l <= cq && !isfinite(u1)) th = -1.0;
                         int li = l;
                         gargmin<P>(th, li);
-                        if (th < 0.0) { NTM_CNT(CN_CDPX_NAN); break; }
-                        if (!(th < kInf)) {                // full step: p joins A
+                        if (th < 0.0) {
+                            NTM_CNT(CN_CDPX_NAN);
+                            if (!kSkipNan || nres >= budget) break;
+                            if (l == 0) w.aflag()[p] |= kSkipRow;
+                            if (l < N) w.U()[l] = w.D()[l] * V0;   // the pick's y at V0, not the end point's
+                            NTM_WSYNC();
+                            ++nskip;
+                            NTM_CNT(CN_CDP_SKIP);
+                            pick = true;
+                            fresh_y = true;
+                        } else if (!(th < kInf)) {         // full step: p joins A
                             if (fk != 2) {
                                 // p's own multiplier < 0 at the end point (A's are all >= 0): p
                                 // (nearly) depends on A, an ill-conditioned step at long horizons.
@@ -4498,11 +4528,13 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                             u0 = (l < cq) ? u1 : 0.0;
                             V0 = vf;
                             pick = true;
+                            clear_skips();
                         } else {                           // partial step: row li reaches u = 0 and leaves
                             V0 += th * (vf - V0);
                             u0 += th * (u1 - u0);
                             drop_at(li, u0);
                             NTM_CNT(CN_CDP_PART);
+                            clear_skips();
                         }
                     } else {                               // dual-only step: n_p = sum_i r_i n_i over A
                         NTM_CNT(CN_CDP_DIR);
@@ -4515,12 +4547,14 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                         if (!(tt < kInf)) { NTM_CNT(CN_CDPX_TINF); break; }   // no row can leave: GI decides (infeasible)
                         u0 -= tt * r;
                         drop_at(li, u0);
+                        clear_skips();
                     }
                     if (pick) {                            // the most violated row at V0 (y of the last re-solve in w.xp())
                         if (l < cq) w.aflag()[w.act()[l]] = kActiveRow;
                         NTM_WSYNC();
                         const double vmx = fmax(1.0, gmax<P>(l < N ? fabs(V0) : 0.0));
-                        const Pick pk = rows.template check<P>(w, V0, l, false, vmx, w.xp());
+                        const Pick pk = rows.template check<P>(w, V0, l, false, vmx, fresh_y ? nullptr : w.xp());
+                        fresh_y = false;
                         NTM_WSYNC();
                         if (l < cq) w.aflag()[w.act()[l]] = 0;
                         NTM_WSYNC();
@@ -4548,6 +4582,7 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                     if (nres > 1) NTM_CNT(CN_REPAIR);
                 } else {
                     NTM_CNT(CN_CDP_GI);
+                    clear_skips();
                     // GI warm from the current set (dual feasible on the primal phase)
                     if (l < cq) {
                         w.aflag()[w.act()[l]] = kCandRow;
