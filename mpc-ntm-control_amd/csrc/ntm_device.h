@@ -1484,13 +1484,35 @@ __device__ __forceinline__ int scale_gram(const W& w, double* G, int l) {
 // what the full G would give); F~ = D F; norms of the scaled state rows
 // ||Gamma_r D||.  Gamma stays unscaled (D is applied on the fly).  The full
 // G~ is only formed when the Goldfarb-Idnani fallback runs (full_gram).
-// Returns false (group-uniform) if any datum is non-finite.
+// Returns (group-uniform) 2 if any datum is non-finite, else 1 if a constant
+// row is violated (the x_0 rows and state rows Gamma does not reach: D15, D22,
+// StructRows::feasible_const's test, folded into the row pass that finds them
+// and into the one reduction, round 6), else 0.
 // ---------------------------------------------------------------------------
+// The far N = 20 build keeps the separate test (qp_phase calls feasible_const):
+// folded in, it cost that kernel 1.3% through register allocation (6.30 -> 6.38 ms)
+// while config 2 (0.201 -> 0.199 ms) and config 5 (74.2 -> 73.7 ms) gained.
+template <class W>
+__device__ __forceinline__ constexpr bool fold_const() { return !(W::kFar && W::kNN == 20); }
 template <int P, class W>
-__device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int l, bool with_state_rows) {
+__device__ __forceinline__ int diag_scale_phase(const Prob& pb, const W& w, int l, bool with_state_rows,
+                                                double x0 = 0.0, double x1 = 0.0) {
     const int N = w.n();
     const OmQ<qi_on<W>()> qw(pb.Q);
-    int bad = 0;
+    int bad = 0, infe = 0;
+    auto const_row = [&](int r) {                         // 0 <= b on a constant state row, to kConstTol
+        if constexpr (!fold_const<W>()) return;
+        const int c = r & 1;
+        const double er = w.e()[r];
+        infe |= (er - pb.xmin[c]) < -kConstTol;
+        infe |= (pb.xmax[c] - er) < -kConstTol;
+    };
+    if (fold_const<W>() && with_state_rows && l == 0) {   // the x_0 rows (D15)
+        infe |= (x0 - pb.xmin[0]) < -kConstTol;
+        infe |= (x1 - pb.xmin[1]) < -kConstTol;
+        infe |= (pb.xmax[0] - x0) < -kConstTol;
+        infe |= (pb.xmax[1] - x1) < -kConstTol;
+    }
     NTM_T0(tsc);
     // Short horizons (2N <= 64, N = 20): the column pass and the row pass each split
     // their sums in two halves at H = ceil(N/2) on otherwise idle lanes, so the wave
@@ -1608,13 +1630,14 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
                 const double ir = (sr > 0.0 && sr < kInf) ? rsqrt_nr(sr) : 0.0;
                 w.irn()[r] = ir;
                 w.rinfo()[r] = (lr + 1) | (cr > 1 ? kRowMulti : 0);
+                if (ir == 0.0) const_row(r);
             }
             NTM_WSYNC();
         }
         NTM_ACC(ST_SC_ROW, tsc);
-        const bool ok = gmaxi<P>(bad) == 0;
+        const int code = fold_const<W>() ? gmaxi<P>(bad ? 2 : infe) : (gmaxi<P>(bad) != 0 ? 2 : 0);
         NTM_ACC(ST_SC_END, tsc);
-        return ok;
+        return code;
     }
     if (l < N) {
         // one pass over Gamma's column l: the Gram diagonal G_ll and F_l = 2 Gamma_l' Om (e - r)
@@ -1696,13 +1719,14 @@ __device__ __forceinline__ bool diag_scale_phase(const Prob& pb, const W& w, int
             const double ir = (s > 0.0 && s < kInf) ? rsqrt_nr(s) : 0.0;
             w.irn()[r] = ir;                     // 1/|Gamma_r D| (0: constant row)
             w.rinfo()[r] = (last + 1) | (cnt > 1 ? kRowMulti : 0);
+            if (ir == 0.0) const_row(r);
         }
         NTM_WSYNC();
     }
     NTM_ACC(ST_SC_ROW, tsc);
-    const bool ok = gmaxi<P>(bad) == 0;
+    const int code = fold_const<W>() ? gmaxi<P>(bad ? 2 : infe) : (gmaxi<P>(bad) != 0 ? 2 : 0);
     NTM_ACC(ST_SC_END, tsc);
-    return ok;
+    return code;
 }
 
 // the full scaled Hessian G~ (lower triangle, WS::gr) for the GI fallback
@@ -4290,7 +4314,8 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
     *qp_iters = 0;
     StructRows rows(pb);
     int* cand = w.cand() + slot * (N + 1);               // this QP's active set is stored here
-    if (!diag_scale_phase<P>(pb, w, l, full)) {
+    const int scode = diag_scale_phase<P>(pb, w, l, full, x0, x1);
+    if (scode >= 2) {
         flag = NTM_EXIT_NONFINITE;
     } else {
         const int nrows = (pb.mode == NTM_MODE_NONE) ? 0 : rows.rows();
@@ -4298,7 +4323,10 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
             for (int i = l; i < nrows; i += P) w.aflag()[i] = 0;
             NTM_WSYNC();
         }
-        if (pb.mode != NTM_MODE_NONE && !rows.template feasible_const<P>(w, x0, x1, l)) {
+        bool infeasible;                                   // a constant row violated (D15, D22)
+        if constexpr (fold_const<W>()) infeasible = pb.mode != NTM_MODE_NONE && scode == 1;
+        else infeasible = pb.mode != NTM_MODE_NONE && !rows.template feasible_const<P>(w, x0, x1, l);
+        if (infeasible) {
             flag = NTM_EXIT_INFEASIBLE;
         } else {
             NTM_ACC(ST_SCALE, tq);
