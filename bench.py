@@ -61,6 +61,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample length")
     ap.add_argument("--small-batch", type=int, default=-1,
                     help="N=20: batches up to this size run on the all-LDS build (-1: library default, 0: never)")
+    ap.add_argument("--one-wave-batch", type=int, default=-1,
+                    help="N=20: all-LDS batches up to this size use the one-wave register budget "
+                         "(-1: library default, 4 x the compute units; 0: never)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="nccl (= RCCL over xGMI) for real runs; gloo only to rehearse the multi-rank "
                          "control flow with more ranks than GPUs (ranks share devices, timing not meaningful)")
@@ -364,6 +367,7 @@ def main():
         pin_layout(ctl, world * B, cfg)
     else:
         ctl.set_small_batch(args.small_batch)
+    ctl.set_one_wave_batch(args.one_wave_batch)
     # shard: global scenario ids [rank*B, (rank+1)*B)  (shard-invariant inputs)
     x0 = ntm_mpc.device_tensor(ntm_mpc.scenarios_x0(rank * B, B), local)
 

@@ -115,6 +115,14 @@ int ntm_ctx_set_stats(ntm_ctx* ctx, int32_t* dev_stats);
  * the two builds agree to the parity tolerances, not bit for bit; within one
  * build a scenario's results do not depend on the batch around it. */
 int ntm_ctx_set_small_batch(ntm_ctx* ctx, int64_t max_scenarios);
+/* Among the all-LDS N = 20 batches, those of at most max_scenarios run with a
+ * one-wave-per-SIMD register budget (round 6): default (and < 0) 4 x the compute
+ * units (1024 on an MI355X: one wave per SIMD), 0 = never.  Bit-identical
+ * results to the two-wave budget; only the speed differs. */
+int ntm_ctx_set_one_wave_batch(ntm_ctx* ctx, int64_t max_scenarios);
+/* The build a step/run launch of B scenarios with cfg takes on this context:
+ * *build = 0 far workspace, 1 all-LDS, 2 all-LDS with the one-wave budget. */
+int ntm_ctx_step_build(const ntm_ctx* ctx, const ntm_config* cfg, int64_t B, int32_t* build);
 /* Which build a step/run launch of B scenarios at horizon N takes on this
  * context: *far = 1 for the far-workspace build, 0 for an all-LDS one. */
 int ntm_ctx_step_layout(const ntm_ctx* ctx, int32_t N, int64_t B, int32_t* far);

@@ -401,6 +401,7 @@ struct ntm_ctx {
     hipEvent_t fbuf_done = nullptr;   // recorded after the last launch that used fbuf
     int cus = 256;                    // compute units of the device (small_batch)
     int64_t near_max = -1;            // ntm_ctx_set_small_batch (< 0: 8 x cus)
+    int64_t near1_max = -1;           // ntm_ctx_set_one_wave_batch (< 0: 4 x cus)
     hipStream_t stream = nullptr;
 };
 
@@ -518,6 +519,14 @@ bool small_batch(const ntm_ctx* ctx, int64_t B) {
         return B <= lim;
     }
 }
+// Among those, batches of at most 4 per CU (one wave per SIMD) take the one-wave
+// register budget of the same build (ntm_n20near1w.hip, bit-identical results)
+template <int NN>
+bool one_wave_batch(const ntm_ctx* ctx, int64_t B) {
+    if (!small_batch<NN>(ctx, B)) return false;
+    const int64_t lim = ctx->near1_max >= 0 ? ctx->near1_max : 4LL * ctx->cus;
+    return B <= lim;
+}
 
 template <int P, int NN>
 int launch_step(ntm_ctx* ctx, Prob pb, int64_t B, const double* x_k, double* rho, double* U_old,
@@ -540,8 +549,11 @@ int launch_step(ntm_ctx* ctx, Prob pb, int64_t B, const double* x_k, double* rho
                                                     active_ws, lds, st)
                             : ntm_launch_step_n50(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters,
                                                   active_ws, lds, st))
-            : near   ? ntm_launch_step_n20near(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters,
-                                               active_ws, lds, st)
+            : near   ? (one_wave_batch<NN>(ctx, B)
+                            ? ntm_launch_step_n20near1w(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag,
+                                                        inner_iters, active_ws, lds, st)
+                            : ntm_launch_step_n20near(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag,
+                                                      inner_iters, active_ws, lds, st))
                      : ntm_launch_step_n20(pb, B, x_k, rho, U_old, U, x_pred, x_next, exitflag, inner_iters, active_ws,
                                            lds, st);
         const int rc = check_hip(ctx, e, "k_mpc_step<64,NN> launch");
@@ -585,7 +597,11 @@ int launch_run(ntm_ctx* ctx, Prob pb, int64_t B, int k_sim, const double* x0, do
             NN == 50 ? (pb.mode == NTM_MODE_FULL_DU
                             ? ntm_launch_run_n50m3(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st)
                             : ntm_launch_run_n50(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st))
-            : near   ? ntm_launch_run_n20near(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st)
+            : near   ? (one_wave_batch<NN>(ctx, B)
+                            ? ntm_launch_run_n20near1w(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds,
+                                                       st)
+                            : ntm_launch_run_n20near(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds,
+                                                     st))
                      : ntm_launch_run_n20(pb, B, k_sim, x0, xk, uk, Uk, wpred, exitflag, inner_iters, lds, st);
         const int rc = check_hip(ctx, e, "k_mpc_run<64,NN> launch");
         return near ? rc : far_release<NN>(ctx, rc, st);
@@ -784,6 +800,24 @@ int ntm_ctx_set_stats(ntm_ctx* ctx, int32_t* dev_stats) {
 int ntm_ctx_set_small_batch(ntm_ctx* ctx, int64_t max_scenarios) {
     if (!ctx) return NTM_E_INVALID;
     ctx->near_max = max_scenarios < 0 ? -1 : max_scenarios;
+    return NTM_OK;
+}
+
+int ntm_ctx_set_one_wave_batch(ntm_ctx* ctx, int64_t max_scenarios) {
+    if (!ctx) return NTM_E_INVALID;
+    ctx->near1_max = max_scenarios < 0 ? -1 : max_scenarios;
+    return NTM_OK;
+}
+
+int ntm_ctx_step_build(const ntm_ctx* ctx, const ntm_config* cfg, int64_t B, int32_t* build) {
+    if (!build) return NTM_E_INVALID;
+    int32_t far = 0, lanes = 0, nn = 0;
+    if (int rc = ntm_ctx_step_layout_cfg(ctx, cfg, B, &far, &lanes, &nn)) return rc;
+#ifndef NTM_SINGLE_TU
+    *build = far ? 0 : ((lanes == 64 && nn == 20 && one_wave_batch<20>(ctx, B)) ? 2 : 1);
+#else
+    *build = far ? 0 : 1;
+#endif
     return NTM_OK;
 }
 

@@ -356,5 +356,6 @@ hipError_t ntm_launch_run_v(const ntm::Prob& pb, int64_t B, int k_sim, const dou
     }
 NTM_DECLARE_LAYOUT_LAUNCHERS(n20)
 NTM_DECLARE_LAYOUT_LAUNCHERS(n20near)
+NTM_DECLARE_LAYOUT_LAUNCHERS(n20near1w)
 NTM_DECLARE_LAYOUT_LAUNCHERS(n50)
 NTM_DECLARE_LAYOUT_LAUNCHERS(n50m3)

@@ -64,6 +64,8 @@ EXPORTS = {
     "ntm_last_error": (C.c_char_p, [C.c_void_p]),
     "ntm_ctx_set_stats": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ntm_ctx_set_small_batch": (C.c_int, [C.c_void_p, C.c_int64]),
+    "ntm_ctx_set_one_wave_batch": (C.c_int, [C.c_void_p, C.c_int64]),
+    "ntm_ctx_step_build": (C.c_int, [C.c_void_p, _CFG, C.c_int64, C.POINTER(C.c_int32)]),
     "ntm_ctx_step_layout": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64, C.POINTER(C.c_int32)]),
     "ntm_ctx_step_layout_cfg": (C.c_int, [C.c_void_p, _CFG, C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                                           C.POINTER(C.c_int32)]),

@@ -251,10 +251,24 @@ class NtmMpc:
 
     def set_small_batch(self, max_scenarios: int = -1):
         """ntm_ctx_set_small_batch: N = 20 batches of at most ``max_scenarios``
-        run on the all-LDS 2-wave build, larger ones on the far-workspace 3-wave
-        build; -1 restores the default (32 x the compute units), 0 always uses
-        the far build."""
+        run on the all-LDS build, larger ones on the far-workspace 4-wave build;
+        -1 restores the default (8 x the compute units), 0 always uses the far
+        build."""
         self._raise(self.lib.ntm_ctx_set_small_batch(self._ctx, int(max_scenarios)), "ntm_ctx_set_small_batch")
+
+    def set_one_wave_batch(self, max_scenarios: int = -1):
+        """ntm_ctx_set_one_wave_batch: all-LDS N = 20 batches of at most
+        ``max_scenarios`` use the one-wave register budget (bit-identical results);
+        -1 restores the default (4 x the compute units), 0 never."""
+        self._raise(self.lib.ntm_ctx_set_one_wave_batch(self._ctx, int(max_scenarios)), "ntm_ctx_set_one_wave_batch")
+
+    def step_build(self, B: int, cfg: Config | None = None) -> str:
+        """The build a launch of B scenarios takes: "far", "lds" or "lds1" (the
+        all-LDS build with the one-wave register budget; ntm_ctx_step_build)."""
+        b = C.c_int32()
+        self._raise(self.lib.ntm_ctx_step_build(self._ctx, C.byref((cfg or self.config).to_c()), int(B), C.byref(b)),
+                    "ntm_ctx_step_build")
+        return ("far", "lds", "lds1")[b.value]
 
     def set_scenarios(self, gen: ScenarioGen | None):
         """Attach a scenario generator (ntm_ctx_set_scenarios): subsequent
@@ -280,7 +294,8 @@ class NtmMpc:
     def step_kernel_name(self, B: int, cfg: Config | None = None) -> str:
         """Name of the fused step kernel specialisation a launch uses (reporting)."""
         layout, lanes, nn = self._layout(B, cfg or self.config)
-        return f"k_mpc_step<P={lanes},NN={nn},{layout}>"
+        build = self.step_build(B, cfg)
+        return f"k_mpc_step<P={lanes},NN={nn},{layout}>" + (" (one-wave budget)" if build == "lds1" else "")
 
     # ------------------------------------------------------------ hot path
     def initial_state(self, x0: torch.Tensor, cfg: Config | None = None):

@@ -329,6 +329,33 @@ def test_small_batch_builds_agree(ctl):
     assert np.max(np.abs(H(a["U"]) - H(b["U"]))) / cfg.umax <= 1e-12
 
 
+def test_one_wave_build_bitwise(ctl):
+    """The all-LDS N = 20 build with the one-wave register budget (batches of at
+    most 4 per CU, ntm_ctx_set_one_wave_batch) is the same arithmetic as the
+    two-wave one: step and closed loop agree bit for bit; the builds are chosen
+    by batch size (one wave up to 4 per CU, two up to 8 per CU, far above)."""
+    B = 64
+    cfg, ocfg = cfgs(20, 2)
+    assert ctl.step_build(1024, cfg) == "lds1" and ctl.step_build(2048, cfg) == "lds"
+    assert ctl.step_build(100_000, cfg) == "far"
+    assert "(one-wave budget)" in ctl.step_kernel_name(1024, cfg)
+    x = O.scenario_x0(np.arange(B)).T
+    rho, Uo = cbind.initial_state(x, ocfg)
+    outs, runs = [], []
+    for lim in (-1, 0):
+        ctl.set_one_wave_batch(lim)
+        try:
+            assert ctl.step_build(B, cfg) == ("lds1" if lim < 0 else "lds")
+            outs.append(ctl.step(T(x), T(rho), T(Uo), cfg))
+            runs.append(ctl.run(T(x), 6, cfg))
+        finally:
+            ctl.set_one_wave_batch(-1)
+    for k in ("U", "x_pred", "x_next", "exitflag", "inner_iters"):
+        assert torch.equal(outs[0][k], outs[1][k]), k
+    for k in ("uk", "Uk", "xk", "wpred", "exitflag", "inner_iters"):
+        assert torch.equal(runs[0][k], runs[1][k]), k
+
+
 def test_sharded_far_total_is_bitwise(ctl):
     """A batch that takes the far build on one GPU (8192 > 2048 scenarios),
     sharded into all-LDS-size shards of 1024 with dist.pin_layout, reproduces
