@@ -1108,8 +1108,28 @@ __device__ __forceinline__ void lift_literal(const Prob& pb, const W& w, const C
     NTM_WSYNC();
 }
 
+#ifndef NTM_FUSE_COLSUM
+#define NTM_FUSE_COLSUM 1  // the slim lift accumulates the scaling pass's column sums (ColSums):
+#endif                     // bit 0 long horizons (N = 50), bit 1 the far N = 20 kernel
+// The scaling pass's column sums, accumulated by the slim lift (NTM_FUSE_COLSUM):
+// lane l < N walks Gamma's column l stage by stage, so it can add G_ll's and F_l's
+// terms as it produces them (the free response e_i is lane N's value at the same
+// stage, read by readlane), instead of the scaling pass reading the column back
+// from LDS.  Same terms in the same order as the pass (diag_scale_phase).  Round 6,
+// A/B on one box: config 5 mode 2 73.9 -> 70.9 ms per step-batch; the far N = 20
+// kernel 6.31 -> 6.50 ms (its register allocation again), so N = 50 only.
+struct ColSums {
+    double s = 0.0, f = 0.0;   // sum_i Gamma_il' Om Gamma_il and sum_i Gamma_il' Om (e_i - r)
+    int bad = 0;               // a non-finite Gamma entry
+};
+template <class W>
+__device__ __forceinline__ constexpr bool fuse_colsum() {
+    return W::kSlim && (W::kNN > 32 ? (NTM_FUSE_COLSUM & 1) != 0 : (NTM_FUSE_COLSUM & 2) != 0);
+}
+
 template <int P, class W>
-__device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l, double x0 = 0.0, double x1 = 0.0) {
+__device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l, double x0 = 0.0, double x1 = 0.0,
+                                           ColSums* cs = nullptr) {
     const int N = w.n();
     const Coef k = scn_coef(pb, w);
     if constexpr (W::kSlim) {
@@ -1136,6 +1156,26 @@ __device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l, do
             double* const rec = gam ? w.Gt() + w.gidx(2 * l, l) - 2 * l : w.e();
             rec[2 * (gam ? l : 0)] = g0;
             rec[2 * (gam ? l : 0) + 1] = g1;
+            // stage i's terms of the column sums (lane N holds e_i): the scaling pass's
+            // and free_response's expressions
+            double cs_s = 0.0, cs_f = 0.0;
+            int cs_bad = 0;
+            const OmQ<qi_on<W>()> cq(pb.Q);
+            auto col_terms = [&](int i) {
+                if constexpr (fuse_colsum<W>()) {
+                    const double e0 = gbcast<P>(g0, N), e1 = gbcast<P>(g1, N);
+                    const double d0 = e0 - pb.r[0], d1 = e1 - pb.r[1];
+                    const double ea = cq.o0(d0, d1), eb = cq.o1(d0, d1);
+                    const double o0 = cq.o0(g0, g1), o1 = cq.o1(g0, g1);
+                    const double t = g0 * o0 + g1 * o1;
+                    const double tf = g0 * ea + g1 * eb;
+                    const bool on = gam && i >= l;
+                    if (on) cs_bad |= !isfinite(g0) || !isfinite(g1);
+                    cs_s += on ? t : 0.0;
+                    cs_f += on ? tf : 0.0;
+                }
+            };
+            col_terms(0);
             constexpr int CH = NTM_CH;
             NTM_CHUNK_PRAGMA
             for (int i0 = 1; i0 < N; i0 += CH) {
@@ -1164,9 +1204,11 @@ __device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l, do
                         const int at = live ? i : l;
                         rec[2 * at] = g0;
                         rec[2 * at + 1] = g1;
+                        col_terms(i);
                     }
                 }
             }
+            if (cs) { cs->s = cs_s; cs->f = cs_f; cs->bad = cs_bad; }
         }
         NTM_ACC(ST_L_LOOP, tlf);
         NTM_WSYNC();
@@ -1496,7 +1538,7 @@ template <class W>
 __device__ __forceinline__ constexpr bool fold_const() { return !(W::kFar && W::kNN == 20); }
 template <int P, class W>
 __device__ __forceinline__ int diag_scale_phase(const Prob& pb, const W& w, int l, bool with_state_rows,
-                                                double x0 = 0.0, double x1 = 0.0) {
+                                                double x0 = 0.0, double x1 = 0.0, const ColSums* cs = nullptr) {
     const int N = w.n();
     const OmQ<qi_on<W>()> qw(pb.Q);
     int bad = 0, infe = 0;
@@ -1645,6 +1687,11 @@ __device__ __forceinline__ int diag_scale_phase(const Prob& pb, const W& w, int 
         const double* om = w.xp();               // Om (e_i - r), from free_response
         double s = 0.0, fs = 0.0;
         constexpr int CH = NTM_CH;
+        if (fuse_colsum<W>() && cs) {           // summed by the lift
+            s = cs->s;
+            fs = cs->f;
+            bad |= cs->bad;
+        } else {
         NTM_CHUNK_PRAGMA
         for (int i0 = 0; i0 < N; i0 += CH) {     // fixed trip count, terms i < l masked; batched loads
             double ga[CH], gb[CH], ea[CH], eb[CH];
@@ -1671,6 +1718,7 @@ __device__ __forceinline__ int diag_scale_phase(const Prob& pb, const W& w, int 
                 s += on ? t : 0.0;
                 fs += on ? tf : 0.0;
             }
+        }
         }
         double g = 2 * s;
         if constexpr (ru_on<W>()) g = g + 2 * pb.Ru;   // G_ll + 2 Ru (ABI v5)
@@ -4305,7 +4353,8 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
     const int N = w.n();
     bool yv = false;                                     // w.xp() holds Gamma U of the final U
     NTM_T0(tq);
-    lift_phase<P>(pb, w, l, x0, x1);
+    ColSums colsum;
+    lift_phase<P>(pb, w, l, x0, x1, &colsum);
     NTM_ACC(ST_LIFT, tq);
     free_response<P>(w, x0, x1, l, &pb);     // F is formed with the Jacobi scaling below
     NTM_ACC(ST_COST, tq);
@@ -4314,7 +4363,7 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
     *qp_iters = 0;
     StructRows rows(pb);
     int* cand = w.cand() + slot * (N + 1);               // this QP's active set is stored here
-    const int scode = diag_scale_phase<P>(pb, w, l, full, x0, x1);
+    const int scode = diag_scale_phase<P>(pb, w, l, full, x0, x1, &colsum);
     if (scode >= 2) {
         flag = NTM_EXIT_NONFINITE;
     } else {

@@ -10,6 +10,6 @@ for r in 1 2; do
   for lib in "${libs[@]}"; do
     tag=$(basename "$lib" .so)
     NTM_MPC_LIB=$lib timeout -k 10 200 python bench.py --no-cpu "$@" > gpurun_out/abm_${tag}_$r.json 2>/dev/null || exit 1
-    python -c "import json; d=json.load(open('gpurun_out/abm_${tag}_$r.json')); print('$tag', $r, round(d['ms_per_step'], 3), d['solver']['optimal_frac'])"
+    python -c "import json; d=json.load(open('gpurun_out/abm_${tag}_$r.json')); print('$tag', $r, round(d['ms_per_step'], 4), d['solver']['optimal_frac'])"
   done
 done

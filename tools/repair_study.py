@@ -64,6 +64,8 @@ class QP:
         self.nnz = np.array([len(c) for c in nzl])
 
     def kind(self, i):
+        if mode == O.MODE_BOX:
+            return 0 if i < N else 1
         if mode == O.MODE_FULL_DU and i >= 6 * N + 4:
             return 4
         if i < 6 * N and i % 6 < 2:
@@ -371,7 +373,14 @@ strategies = {
     "GI: delta cand + hint shift(p10)": lambda q, c, a: gi_resolve(q, HINTS.get("dc", c), a, 64, hint=HINTS.get("s10")),
     "PDAS (8)": lambda q, c, a: pdas(q, c, None, 8),
     "PDAS (2) then GI path": lambda q, c, a: pdas_then_gi(q, c, 2),
+    # box-only QPs (mode 1, BASELINE config 2): the kernel's 16 single-row exchanges vs PDAS
+    "device (16 exchanges)": lambda q, c, a: device_repair(q, c, None, 16),
+    "PDAS (16)": lambda q, c, a: pdas(q, c, None, 16),
 }
+import os  # noqa: E402
+if os.environ.get("STRATS"):                     # e.g. STRATS="device (16,PDAS (16"
+    keys = os.environ["STRATS"].split(",")
+    strategies = {k: f for k, f in strategies.items() if any(k.startswith(p) for p in keys)}
 res = {it: {k: [0, 0, 0] for k in strategies} for it in ITERS}   # certified, re-solves, count
 exact = {it: 0 for it in ITERS}
 first_fail = {it: 0 for it in ITERS}
@@ -430,5 +439,7 @@ for it in ITERS:
     print(f"N={N} mode={mode} iteration {it}: {cnt} QPs, steps {lo}-{hi}, {S} scenarios; candidate exact {exact[it] / cnt:.2f}, first try fails {first_fail[it] / cnt:.2f}")
     for name, (ok, n, c) in res[it].items():
         print(f"  {name:30s} certified {ok / cnt:.3f}  GI {1 - ok / cnt:.3f}  re-solves {n / cnt:.2f}")
-    h = np.array(hist[it])
+    h = np.array(hist[it], dtype=np.int64)
+    if not len(h):
+        continue
     print("  GI by re-solves (64): re-solve counts of certified QPs", np.bincount(h[h > 0]).tolist(), "failed", int((h < 0).sum()))
