@@ -1108,23 +1108,29 @@ __device__ __forceinline__ void lift_literal(const Prob& pb, const W& w, const C
     NTM_WSYNC();
 }
 
+#ifndef NTM_ROW_PAIRS
+#define NTM_ROW_PAIRS 0    // 1: long horizons, the scaling pass's row norms two rows per lane (slower)
+#endif
 #ifndef NTM_FUSE_COLSUM
-#define NTM_FUSE_COLSUM 1  // the slim lift accumulates the scaling pass's column sums (ColSums):
-#endif                     // bit 0 long horizons (N = 50), bit 1 the far N = 20 kernel
+#define NTM_FUSE_COLSUM 1  // the lift accumulates the scaling pass's column sums (ColSums): bit 0
+#endif                     // long horizons (N = 50), bit 1 the far N = 20 kernel, bit 2 the all-LDS N = 20 one
 // The scaling pass's column sums, accumulated by the slim lift (NTM_FUSE_COLSUM):
 // lane l < N walks Gamma's column l stage by stage, so it can add G_ll's and F_l's
 // terms as it produces them (the free response e_i is lane N's value at the same
 // stage, read by readlane), instead of the scaling pass reading the column back
 // from LDS.  Same terms in the same order as the pass (diag_scale_phase).  Round 6,
 // A/B on one box: config 5 mode 2 73.9 -> 70.9 ms per step-batch; the far N = 20
-// kernel 6.31 -> 6.50 ms (its register allocation again), so N = 50 only.
+// kernel 6.31 -> 6.50 ms (its register allocation again) and the all-LDS one (config
+// 2 0.193 -> 0.210 ms: e_i takes six lane reads there), so N = 50 only.
 struct ColSums {
     double s = 0.0, f = 0.0;   // sum_i Gamma_il' Om Gamma_il and sum_i Gamma_il' Om (e_i - r)
     int bad = 0;               // a non-finite Gamma entry
 };
 template <class W>
 __device__ __forceinline__ constexpr bool fuse_colsum() {
-    return W::kSlim && (W::kNN > 32 ? (NTM_FUSE_COLSUM & 1) != 0 : (NTM_FUSE_COLSUM & 2) != 0);
+    if constexpr (W::kSlim) return W::kNN > 32 ? (NTM_FUSE_COLSUM & 1) != 0 : (NTM_FUSE_COLSUM & 2) != 0;
+    // the all-LDS N = 20 build (lanes N, N+1 and N+2 hold Phi's columns and Lambda)
+    else return !W::kFar && W::kNN == 20 && (NTM_FUSE_COLSUM & 4) != 0;
 }
 
 template <int P, class W>
@@ -1251,6 +1257,31 @@ __device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l, do
             rec[st * i + 1] = g1;
         };
         put(gam ? l : 0);
+        // stage i's terms of the scaling pass's column sums (ColSums): e_i = Phi_i x_k +
+        // Lambda_i from lanes N, N+1 (Phi's columns) and N+2 (Lambda), free_response's
+        // expressions
+        double cs_s = 0.0, cs_f = 0.0;
+        int cs_bad = 0;
+        const OmQ<qi_on<W>()> cq(pb.Q);
+        auto col_terms = [&](int i) {
+            if constexpr (fuse_colsum<W>()) {
+                const double p00 = gbcast<P>(g0, N), p10 = gbcast<P>(g1, N);
+                const double p01 = gbcast<P>(g0, N + 1), p11 = gbcast<P>(g1, N + 1);
+                const double l0 = gbcast<P>(g0, N + 2), l1 = gbcast<P>(g1, N + 2);
+                const double e0 = (p00 * x0 + p01 * x1) + l0;
+                const double e1 = (p10 * x0 + p11 * x1) + l1;
+                const double d0 = e0 - pb.r[0], d1 = e1 - pb.r[1];
+                const double ea = cq.o0(d0, d1), eb = cq.o1(d0, d1);
+                const double o0 = cq.o0(g0, g1), o1 = cq.o1(g0, g1);
+                const double t = g0 * o0 + g1 * o1;
+                const double tf = g0 * ea + g1 * eb;
+                const bool on = gam && i >= l;
+                if (on) cs_bad |= !isfinite(g0) || !isfinite(g1);
+                cs_s += on ? t : 0.0;
+                cs_f += on ? tf : 0.0;
+            }
+        };
+        col_terms(0);
         // fixed trip count (unrolls), branch-free: Gamma rows i <= l keep (B_l, 0) and
         // rewrite the diagonal.  The coefficients of CH steps are loaded ahead of the
         // chunk's stores (the stores cannot be proven not to alias them, so per-step
@@ -1276,9 +1307,11 @@ __device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l, do
                     g0 = live ? n0 : g0;
                     g1 = live ? n1 : g1;
                     put(live ? i : l);
+                    col_terms(i);
                 }
             }
         }
+        if (cs) { cs->s = cs_s; cs->f = cs_f; cs->bad = cs_bad; }
     }
     NTM_ACC(ST_L_LOOP, tlf);
     // Phi and Lambda on lane 0 when the group has no idle lanes
@@ -1575,7 +1608,10 @@ __device__ __forceinline__ int diag_scale_phase(const Prob& pb, const W& w, int 
         double s = 0.0, fs = 0.0;
         const int col = l < N ? l : l - N;
         const int base = l < N ? 0 : Hs;
-        if (l < (kSC ? 2 * N : N)) {
+        const bool fc = fuse_colsum<W>() && cs != nullptr;   // summed by the lift (one sequential sum)
+        if (fc) {
+            if (l < N) { s = cs->s; fs = cs->f; bad |= cs->bad; }
+        } else if (l < (kSC ? 2 * N : N)) {
             const double* cj = w.Gt() + w.gidx(2 * col, col) - 2 * col;
             const double* om = w.xp();
             constexpr int CH = NTM_CH;
@@ -1607,14 +1643,14 @@ __device__ __forceinline__ int diag_scale_phase(const Prob& pb, const W& w, int 
                 }
             }
         }
-        const double s2 = kSC ? __shfl(s, (l + N) & 63, 64) : 0.0;
-        const double f2 = kSC ? __shfl(fs, (l + N) & 63, 64) : 0.0;
+        const double s2 = (kSC && !fc) ? __shfl(s, (l + N) & 63, 64) : 0.0;
+        const double f2 = (kSC && !fc) ? __shfl(fs, (l + N) & 63, 64) : 0.0;
         if (l < N) {
-            double g = kSC ? 2 * (s + s2) : 2 * s;
+            double g = (kSC && !fc) ? 2 * (s + s2) : 2 * s;
             if constexpr (ru_on<W>()) g = g + 2 * pb.Ru;   // G_ll + 2 Ru (ABI v5)
             const double Dl = (g > 0.0 && g < kInf) ? rsqrt_nr(g) : 1.0;
             w.D()[l] = Dl;
-            const double f = (kSC ? 2 * (fs + f2) : 2 * fs) * Dl;
+            const double f = ((kSC && !fc) ? 2 * (fs + f2) : 2 * fs) * Dl;
             bad |= !isfinite(f) || !isfinite(Dl);
             w.F()[l] = f;
             if constexpr (!W::kSlim) {
@@ -1739,7 +1775,52 @@ __device__ __forceinline__ int diag_scale_phase(const Prob& pb, const W& w, int 
         const double a = w.D()[l], b = w.D()[l - 1];
         w.idun()[l] = 1.0 / sqrt(a * a + b * b);
     }
-    if (with_state_rows) {
+    // Long horizons (P < 2N <= 2P): lane l takes state rows l and l + P in one pass
+    // (both rows' loads of a chunk issued together, D_j loaded once) instead of two
+    // passes (NTM_ROW_PAIRS).  Each row's terms are summed in the same order as below.
+    constexpr bool kRowPairs = NTM_ROW_PAIRS && P == 64 && W::kNN > 32 && W::kNN <= 64;
+    if (kRowPairs && with_state_rows) {
+        const int r1 = l, r2 = l + P;
+        const bool two = r2 < 2 * N;
+        const int jmax1 = r1 >> 1, jmax2 = two ? (r2 >> 1) : -1;
+        double s1 = 0.0, s2 = 0.0;
+        int last1 = -1, cnt1 = 0, last2 = -1, cnt2 = 0;
+        constexpr int CH = NTM_CH;
+        NTM_CHUNK_PRAGMA
+        for (int j0 = 0; j0 < N; j0 += CH) {     // fixed trip count, j > jmax masked; batched loads
+            double g1[CH], g2[CH], dd[CH];
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const int j = j0 + u;
+                g1[u] = j < N ? w.gt(r1, j) : 0.0;
+                g2[u] = (two && j < N) ? w.gt(r2, j) : 0.0;
+                dd[u] = j < N ? w.D()[j] : 0.0;
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < CH; ++u) {
+                const double v1 = g1[u] * dd[u], v2 = g2[u] * dd[u];
+                const bool in1 = j0 + u <= jmax1, in2 = j0 + u <= jmax2;
+                s1 += in1 ? v1 * v1 : 0.0;
+                s2 += in2 ? v2 * v2 : 0.0;
+                if (in1 && g1[u] != 0.0) { last1 = j0 + u; ++cnt1; }
+                if (in2 && g2[u] != 0.0) { last2 = j0 + u; ++cnt2; }
+            }
+        }
+        bad |= !isfinite(s1) || !isfinite(w.e()[r1]);
+        const double ir1 = (s1 > 0.0 && s1 < kInf) ? rsqrt_nr(s1) : 0.0;
+        w.irn()[r1] = ir1;
+        w.rinfo()[r1] = (last1 + 1) | (cnt1 > 1 ? kRowMulti : 0);
+        if (ir1 == 0.0) const_row(r1);
+        if (two) {
+            bad |= !isfinite(s2) || !isfinite(w.e()[r2]);
+            const double ir2 = (s2 > 0.0 && s2 < kInf) ? rsqrt_nr(s2) : 0.0;
+            w.irn()[r2] = ir2;
+            w.rinfo()[r2] = (last2 + 1) | (cnt2 > 1 ? kRowMulti : 0);
+            if (ir2 == 0.0) const_row(r2);
+        }
+        NTM_WSYNC();
+    } else if (with_state_rows) {
         for (int r = l; r < 2 * N; r += P) {
             double s = 0.0;
             const int jmax = r >> 1;
