@@ -192,7 +192,7 @@ enum { ST_LIFT, ST_COST, ST_SCALE, ST_CAND, ST_REGRAM, ST_GI, ST_POLISH, ST_ROLL
        CN_CDPX_SING0, CN_CDPX_SING1, CN_CDPX_BUDGET, CN_CDPX_DIR, CN_CDPX_NOVIOL, CN_CDPX_FULLDUAL, CN_CDPX_TINF,
        CN_BORD_K0, CN_BORD_K1, CN_BORD_K2, CN_BORD_K3, CN_BORD_K4P, CN_SQ_K0, CN_SQ_K1, CN_SQ_K2, CN_SQ_COLL,
        CN_CDPX_NAN, CN_NAN_BORD, CN_NAN_K0, CN_NAN_K1, CN_NAN_K2, CN_NAN_COLL, CN_NAN_COLL2, CN_NAN_PRIMFAIL,
-       CN_NAN_V, CN_BX_O1, CN_BX_O2, CN_BX_O3P, CN_BX_NEG, CN_BX_NOCLASS, CN_CDP_SKIP };
+       CN_NAN_V, CN_BX_O1, CN_BX_O2, CN_BX_O3P, CN_BX_NEG, CN_BX_NOCLASS, CN_CDP_SKIP, CN_CDP_SKIPDIR };
 constexpr double kDepTol = 1e-8;   // GI linear-dependence threshold (oracle GI_DEP_TOL)
 #ifndef NTM_MAX_NT
 #define NTM_MAX_NT 32
@@ -233,6 +233,9 @@ constexpr int kCdpExtra = NTM_CDP_EXTRA;
 // the dual path's skip of a row whose A + {p} end point is non-finite (long horizons)
 #ifndef NTM_CDP_SKIP
 #define NTM_CDP_SKIP 1
+#endif
+#ifndef NTM_CDP_SKIPDIR
+#define NTM_CDP_SKIPDIR 1  // long horizons: no violated row but skipped ones -> the last one's dual-only step
 #endif
 #ifndef NTM_CDP_HINT
 #define NTM_CDP_HINT 1
@@ -4533,6 +4536,7 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                 // once A changes.  Before round 6 these QPs went to GI (N = 50 mode 2: 0.1 per
                 // MPC step, 7% of the cycles)
                 constexpr bool kSkipNan = NTM_CDP_SKIP && (W::kNN > 32 || W::kNN == 0);
+                constexpr bool kSkipDir = kSkipNan && NTM_CDP_SKIPDIR;
                 int nskip = 0;
                 bool fresh_y = false;                      // the pick recomputes y = Gamma U at V0
                 auto clear_skips = [&]() {
@@ -4716,7 +4720,21 @@ __device__ __forceinline__ int qp_phase(const Prob& pb, const W& w, double x0, d
                         NTM_WSYNC();
                         if (l < cq) w.aflag()[w.act()[l]] = 0;
                         NTM_WSYNC();
-                        if (pk.p < 0 || !(pk.s < -1e-9 * fmax(vmx, fabs(pk.bc)))) { NTM_CNT(CN_CDPX_NOVIOL); break; }
+                        if (pk.p < 0 || !(pk.s < -1e-9 * fmax(vmx, fabs(pk.bc)))) {
+                            // the only violated rows left are skipped ones (A + {p} had a
+                            // non-finite end point: p nearly depends on A): GI's step for a
+                            // dependent row, the dual-only direction of the last skipped row p
+                            // (round 6, NTM_CDP_SKIPDIR), instead of handing the QP to GI
+                            if (kSkipDir && nskip > 0 && p >= 0 && nres < budget) {
+                                NTM_CNT(CN_CDP_SKIPDIR);
+                                dirp = p;
+                                qs = cq;
+                                stage = 3;
+                                continue;
+                            }
+                            NTM_CNT(CN_CDPX_NOVIOL);
+                            break;
+                        }
                         p = pk.p;
                     }
                     if (nres >= budget) { NTM_CNT(CN_CDPX_BUDGET); break; }   // add p: A + {p}, or its direction when A is full

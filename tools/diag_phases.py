@@ -68,7 +68,7 @@ print(f"re-solves with non-finite multipliers per wave-step, by path: bordered {
 print(f"bordered re-solves by shape per wave-step: not classified (nS = 0 or k >= 3) {buf[101]/B:.3f}, "
       f"a row with no free column {buf[100]/B:.3f}, one row left out {buf[97]/B:.3f}, two {buf[98]/B:.3f}, "
       f"three or more {buf[99]/B:.3f}")
-print(f"dual path: rows skipped after a non-finite end point {buf[102]/B:.3f} per wave-step")
+print(f"dual path: rows skipped after a non-finite end point {buf[102]/B:.3f} per wave-step, dual-only steps of a skipped row {buf[103]/B:.3f}")
 print(f"re-solve paths per wave-step: echelon k=0 {buf[84]/B:.2f}, k=1 {buf[85]/B:.2f}, k=2 {buf[86]/B:.2f}, one collision {buf[87]/B:.2f}; "
       f"bordered with k = nF - nS = 0 {buf[79]/B:.2f}, 1 {buf[80]/B:.2f}, 2 {buf[81]/B:.2f}, 3 {buf[82]/B:.2f}, >= 4 {buf[83]/B:.2f}")
 print(f"first tries at it<=2 that failed, by kind, per wave-step: dual {buf[62]/B:.3f}, primal {buf[63]/B:.3f}, "
