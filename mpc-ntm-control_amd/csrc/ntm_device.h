@@ -234,6 +234,9 @@ constexpr int kCdpExtra = NTM_CDP_EXTRA;
 #ifndef NTM_CDP_SKIP
 #define NTM_CDP_SKIP 1
 #endif
+#ifndef NTM_CY_LATE
+#define NTM_CY_LATE 1      // long horizons: Gamma U_B at an echelon set's general rows only (polish_compact)
+#endif
 #ifndef NTM_CDP_SKIPDIR
 #define NTM_CDP_SKIPDIR 1  // long horizons: no violated row but skipped ones -> the last one's dual-only step
 #endif
@@ -2987,6 +2990,11 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
     // all-LDS and generic builds; the far N = 20 / 50 kernels keep one code path)
     constexpr bool kFixedY = !W::kFar;
     const bool allfixed = kFixedY && nF == 0 && nS == 0;
+    // Long horizons (NTM_CY_LATE): the pass runs after the set's shape is known; an
+    // echelon set needs Gamma_r U_B only at its active general rows (h), at most N < P
+    // of them, so one trip over those rows replaces two over all 2N (z = y_B + e - r,
+    // which only the bordered path's g_F reads, is not formed)
+    constexpr bool kLateY = NTM_CY_LATE && W::kNN > 32 && P == 64 && !kSplitR;
     if constexpr (kSplitR) {
         if (!dir) {
             double y[1];
@@ -2996,7 +3004,7 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 w.xp()[l] = allfixed ? y[0] : y[0] + w.e()[l] - ((l & 1) ? pb.r[1] : pb.r[0]);
             }
         }
-    } else {
+    } else if constexpr (!kLateY) {
         for (int r = l; r < 2 * N && !dir; r += P) {
             const double y = gamma_row_dot<NTM_CH>(w, r, w.dr());
             w.Phi()[r] = y;
@@ -3130,6 +3138,23 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 }
                 NTM_WSYNC();
             }
+        }
+    }
+    if constexpr (kLateY) {
+        if (!dir) {
+            if (sq) {
+                if (l < nS) {
+                    const int r = w.srw()[l];
+                    if (r < 2 * N) w.Phi()[r] = gamma_row_dot<NTM_CH>(w, r, w.dr());
+                }
+            } else {
+                for (int r = l; r < 2 * N; r += P) {
+                    const double y = gamma_row_dot<NTM_CH>(w, r, w.dr());
+                    w.Phi()[r] = y;
+                    w.xp()[r] = allfixed ? y : y + w.e()[r] - ((r & 1) ? pb.r[1] : pb.r[0]);
+                }
+            }
+            NTM_WSYNC();
         }
     }
     NTM_ACC(ST_C_SQ, tp);
