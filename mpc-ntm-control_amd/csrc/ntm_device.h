@@ -234,6 +234,12 @@ constexpr int kCdpExtra = NTM_CDP_EXTRA;
 #ifndef NTM_CDP_SKIP
 #define NTM_CDP_SKIP 1
 #endif
+#ifndef NTM_SUB_LANEIDX
+#define NTM_SUB_LANEIDX 0  // 1: the certificate's sparse pass takes rows and z by readlane (long horizons;
+#endif                     // on in the mode-3 TU: 76.9 -> 76.3 ms, while mode 2 ran 64.9 -> 65.6 ms)
+#ifndef NTM_E_LANEIDX
+#define NTM_E_LANEIDX 1    // row-per-lane E build: pivot columns' variables and D_j by readlane
+#endif
 #ifndef NTM_CY_LATE
 #define NTM_CY_LATE 1      // long horizons: Gamma U_B at an echelon set's general rows only (polish_compact)
 #endif
@@ -3291,6 +3297,26 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         // per-lane loop below issues ~5 dependent loads per entry, n^2 / 64 times per
         // lane (n ~ 43 at N = 50).  Entries as gen_n computes them, bit for bit.
         constexpr bool kRowE = W::kNN > 32 || W::kNN == 0 || NTM_ROWE_ALL;
+        // (NTM_E_LANEIDX, P = 64) lane u first loads pivot column u's variable and D_j, and
+        // each row's loop takes them by readlane: one LDS round trip per batch (Gamma_rj)
+        // instead of two (the column index, then Gamma_rj and D_j at it)
+        constexpr bool kLaneIdx = NTM_E_LANEIDX && P == 64;
+        int jfl = 0;
+        double dfl = 0.0;
+        if constexpr (kRowE && kLaneIdx) {
+            if (l < n) {
+                jfl = w.fidx()[pc(l)];
+                dfl = w.D()[jfl];
+            }
+        }
+        auto col_of = [&](int u) -> int {                     // pivot column u's variable (u uniform)
+            if constexpr (kLaneIdx) return __builtin_amdgcn_readlane(jfl, u);
+            else return w.fidx()[pc(u)];
+        };
+        auto d_of = [&](int u, int j) -> double {             // D at it
+            if constexpr (kLaneIdx) return gbcast<P>(dfl, u);
+            else return w.D()[j];
+        };
         if constexpr (kRowE) {
             if (l < n) {
                 const int s2 = perm[l];
@@ -3302,9 +3328,10 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                     const int i = r - 2 * N;
                     const double ir = w.idun()[i];
                     for (int u = 0; u <= l; ++u) {
-                        const int j = w.fidx()[pc(u)];
+                        const int uu = kLaneIdx ? __builtin_amdgcn_readfirstlane(u) : u;
+                        const int j = col_of(uu);
                         const double lv = (j == i) ? sg : (j == i - 1 ? -sg : 0.0);
-                        erow[u] = -((lv * w.D()[j]) * ir);
+                        erow[u] = -((lv * d_of(uu, j)) * ir);
                     }
                 } else {
                     const double ir = w.irn()[r];
@@ -3313,13 +3340,18 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                     for (int u0 = 0; u0 <= l; u0 += CH) {
                         int jj[CH];
                         double g[CH], d[CH];
+                        const int ub = kLaneIdx ? __builtin_amdgcn_readfirstlane(u0) : u0;
 #pragma unroll
-                        for (int c = 0; c < CH; ++c) jj[c] = (u0 + c <= l) ? w.fidx()[pc(u0 + c)] : 0;
+                        for (int c = 0; c < CH; ++c) {
+                            if constexpr (kLaneIdx) jj[c] = col_of((ub + c) & 63);     // lanes >= n hold 0
+                            else jj[c] = (u0 + c <= l) ? w.fidx()[pc(u0 + c)] : 0;
+                        }
 #pragma unroll
                         for (int c = 0; c < CH; ++c) {
                             const bool in = u0 + c <= l && jj[c] <= jm;
                             g[c] = in ? gr[w.gidx(0, jj[c])] : 0.0;
-                            d[c] = (u0 + c <= l) ? w.D()[jj[c]] : 0.0;
+                            if constexpr (kLaneIdx) d[c] = (u0 + c <= l) ? d_of((ub + c) & 63, 0) : 0.0;
+                            else d[c] = (u0 + c <= l) ? w.D()[jj[c]] : 0.0;
                         }
                         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -4041,11 +4073,18 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         // pass over the nS active general rows only (z_s scratch in w.Phi(), dead
         // until the next lift; rows r_s >= 2N are rate rows, handled directly)
         double* const z = w.Phi();
+        // (NTM_SUB_LANEIDX, long horizons) row s's index and z_s stay on lane s and the
+        // column loop takes them by readlane: one LDS round trip per batch instead of two
+        constexpr bool kSubLane = NTM_SUB_LANEIDX && P == 64 && (W::kNN > 32 || W::kNN == 0);
+        int rsl = 0;
+        double zsl = 0.0;
         if (l < nS) {
             const int r = w.srw()[l];
-            z[l] = (r < 2 * N) ? (w.np()[l] * w.ssg()[l]) * w.irn()[r] : 0.0;
+            const double zl = (r < 2 * N) ? (w.np()[l] * w.ssg()[l]) * w.irn()[r] : 0.0;
+            if constexpr (kSubLane) { rsl = r; zsl = zl; }
+            else z[l] = zl;
         }
-        NTM_WSYNC();
+        if constexpr (!kSubLane) NTM_WSYNC();
         if (l < N) {
             const double* cl = w.Gt() + w.gidx(2 * l, l) - 2 * l;   // cl[r] = gt(r, l), r >= 2l
             double sub = 0.0;
@@ -4057,8 +4096,14 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
 #pragma unroll
                 for (int u = 0; u < CH; ++u) {
                     const bool in = s0 + u < nS;
-                    rr[u] = in ? w.srw()[s0 + u] : 0;
-                    zv[u] = in ? z[s0 + u] : 0.0;
+                    if constexpr (kSubLane) {
+                        const int src = __builtin_amdgcn_readfirstlane(s0 + u) & 63;
+                        rr[u] = in ? __builtin_amdgcn_readlane(rsl, src) : 0;
+                        zv[u] = in ? gbcast<P>(zsl, src) : 0.0;
+                    } else {
+                        rr[u] = in ? w.srw()[s0 + u] : 0;
+                        zv[u] = in ? z[s0 + u] : 0.0;
+                    }
                 }
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll

@@ -14,6 +14,11 @@
 #ifndef NTM_COLL3
 #define NTM_COLL3 1
 #endif
+// the certificate's sparse pass over the active general rows by readlane (round 6: mode 3
+// 76.9 -> 76.3 ms per step-batch; the modes 0-2 TU ran 64.9 -> 65.6 ms with it, so off there)
+#ifndef NTM_SUB_LANEIDX
+#define NTM_SUB_LANEIDX 1
+#endif
 #include "ntm_step.h"
 
 NTM_DEFINE_LAYOUT_LAUNCHERS(n50m3, 50, true)
