@@ -234,6 +234,9 @@ constexpr int kCdpExtra = NTM_CDP_EXTRA;
 #ifndef NTM_CDP_SKIP
 #define NTM_CDP_SKIP 1
 #endif
+#ifndef NTM_SUB_AHEAD
+#define NTM_SUB_AHEAD 1    // long horizons: steps ahead the echelon forward substitution loads E
+#endif
 #ifndef NTM_SUB_LANEIDX
 #define NTM_SUB_LANEIDX 0  // 1: the certificate's sparse pass takes rows and z by readlane (long horizons;
 #endif                     // on in the mode-3 TU: 76.9 -> 76.3 ms, while mode 2 ran 64.9 -> 65.6 ms)
@@ -3388,10 +3391,19 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         // E_p V_p = h and (k = 1) E_p Z_p = -e_c: lane t owns row t; step t broadcasts
         // x_t (z_t) and updates the rows below
         double x = 0.0, zz = 0.0, zz2 = 0.0, zz3 = 0.0;
-        double en = (l > 0 && l < n) ? Ep[w.eidx(l, 0)] : 0.0;   // E[l][t], loaded one step ahead
+        // E[l][t] loaded kAhead steps ahead (a register queue; long horizons: NTM_SUB_AHEAD)
+        constexpr int kAhead = (W::kNN > 32) ? NTM_SUB_AHEAD : 1;
+        double eq[kAhead];
+#pragma unroll
+        for (int a = 0; a < kAhead; ++a) eq[a] = (a < n && l > a && l < n) ? Ep[w.eidx(l, a)] : 0.0;
         for (int t = 0; t < n; ++t) {
-            const double et = en;
-            if (t + 1 < n) en = (l > t + 1 && l < n) ? Ep[w.eidx(l, t + 1)] : 0.0;
+            const double et = eq[0];
+#pragma unroll
+            for (int a = 0; a + 1 < kAhead; ++a) eq[a] = eq[a + 1];
+            {
+                const int ta = t + kAhead;
+                eq[kAhead - 1] = (ta < n && l > ta && l < n) ? Ep[w.eidx(l, ta)] : 0.0;
+            }
             const double xt = gbcast<P>(acc * sq_id, t);
             if (l == t) x = xt;
             acc -= et * xt;
