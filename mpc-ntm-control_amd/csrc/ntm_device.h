@@ -234,6 +234,12 @@ constexpr int kCdpExtra = NTM_CDP_EXTRA;
 #ifndef NTM_CDP_SKIP
 #define NTM_CDP_SKIP 1
 #endif
+#ifndef NTM_FUSE_LOCAL_E
+#define NTM_FUSE_LOCAL_E 0 // 1: the fused column sums run the free-response recursion on every lane
+#endif
+#ifndef NTM_MU_AHEAD
+#define NTM_MU_AHEAD 0     // long horizons: steps ahead the multipliers' back substitution loads E (0: none)
+#endif
 #ifndef NTM_SUB_AHEAD
 #define NTM_SUB_AHEAD 1    // long horizons: steps ahead the echelon forward substitution loads E
 #endif
@@ -1182,9 +1188,14 @@ __device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l, do
             double cs_s = 0.0, cs_f = 0.0;
             int cs_bad = 0;
             const OmQ<qi_on<W>()> cq(pb.Q);
+            // NTM_FUSE_LOCAL_E: every lane runs lane N's free-response recursion itself (the
+            // same operations on the same coefficients), so e_i needs no lane read per stage
+            constexpr bool kLocalE = fuse_colsum<W>() && NTM_FUSE_LOCAL_E;
+            double ee0 = kLocalE ? (a0 * x0 + k.C1) : 0.0;
+            double ee1 = kLocalE ? ((c0v * x0 + k.a22 * x1) + k.C2) : 0.0;
             auto col_terms = [&](int i) {
                 if constexpr (fuse_colsum<W>()) {
-                    const double e0 = gbcast<P>(g0, N), e1 = gbcast<P>(g1, N);
+                    const double e0 = kLocalE ? ee0 : gbcast<P>(g0, N), e1 = kLocalE ? ee1 : gbcast<P>(g1, N);
                     const double d0 = e0 - pb.r[0], d1 = e1 - pb.r[1];
                     const double ea = cq.o0(d0, d1), eb = cq.o1(d0, d1);
                     const double o0 = cq.o0(g0, g1), o1 = cq.o1(g0, g1);
@@ -1225,6 +1236,12 @@ __device__ __forceinline__ void lift_phase(const Prob& pb, const W& w, int l, do
                         const int at = live ? i : l;
                         rec[2 * at] = g0;
                         rec[2 * at + 1] = g1;
+                        if constexpr (kLocalE) {
+                            const double m0 = ca[u] * ee0 + k.C1;
+                            const double m1 = (cb[u] * ee0 + k.a22 * ee1) + k.C2;
+                            ee0 = m0;
+                            ee1 = m1;
+                        }
                         col_terms(i);
                     }
                 }
@@ -4011,8 +4028,25 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
             // one collision: a second right-hand side, the left-out row B at the pivot columns
             double acb = (kCollision && xb >= 0 && l < n) ? gen_n(xb, w.fidx()[pl]) : 0.0, mb = 0.0;
             double acb2 = (kColl2 && xb2 >= 0 && l < n) ? gen_n(xb2, w.fidx()[pl]) : 0.0, mb2 = 0.0;
+            // E[u][l] loaded kAheadB steps ahead (long horizons: NTM_MU_AHEAD; a register queue)
+            constexpr int kAheadB = (W::kNN > 32) ? NTM_MU_AHEAD : 0;
+            double bq[kAheadB > 0 ? kAheadB : 1];
+#pragma unroll
+            for (int a = 0; a < kAheadB; ++a) {
+                const int ua = n - 1 - a;
+                bq[a] = (ua >= 0 && l < ua) ? w.Ep()[w.eidx(ua, l)] : 0.0;
+            }
             for (int u = n - 1; u >= 0; --u) {
-                const double eu = (l < u) ? w.Ep()[w.eidx(u, l)] : 0.0;
+                double eu;
+                if constexpr (kAheadB > 0) {
+                    eu = bq[0];
+#pragma unroll
+                    for (int a = 0; a + 1 < kAheadB; ++a) bq[a] = bq[a + 1];
+                    const int ua = u - kAheadB;
+                    bq[kAheadB - 1] = (ua >= 0 && l < ua) ? w.Ep()[w.eidx(ua, l)] : 0.0;
+                } else {
+                    eu = (l < u) ? w.Ep()[w.eidx(u, l)] : 0.0;
+                }
                 const double mu_u = gbcast<P>(acc * sq_id, u);
                 if (l == u) mu = mu_u;
                 acc -= eu * mu_u;
