@@ -237,6 +237,9 @@ constexpr int kCdpExtra = NTM_CDP_EXTRA;
 #ifndef NTM_FUSE_LOCAL_E
 #define NTM_FUSE_LOCAL_E 0 // 1: the fused column sums run the free-response recursion on every lane
 #endif
+#ifndef NTM_SUB_PRESCALE
+#define NTM_SUB_PRESCALE 0 // 1: long horizons, echelon substitutions on accumulators scaled by 1/E[l][l] (slower)
+#endif
 #ifndef NTM_MU_AHEAD
 #define NTM_MU_AHEAD 0     // long horizons: steps ahead the multipliers' back substitution loads E (0: none)
 #endif
@@ -3413,29 +3416,34 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
         double eq[kAhead];
 #pragma unroll
         for (int a = 0; a < kAhead; ++a) eq[a] = (a < n && l > a && l < n) ? Ep[w.eidx(l, a)] : 0.0;
+        // NTM_SUB_PRESCALE (long horizons): the accumulators carry acc / E[l][l] and the
+        // update uses E[l][t] / E[l][l], formed off the chain, so step t's broadcast waits
+        // on one operation less (fma -> readlane -> fma)
+        constexpr bool kPre = NTM_SUB_PRESCALE && W::kNN > 32;
+        if constexpr (kPre) { acc *= sq_id; acz *= sq_id; acz2 *= sq_id; acz3 *= sq_id; }
         for (int t = 0; t < n; ++t) {
-            const double et = eq[0];
+            const double et = kPre ? eq[0] * sq_id : eq[0];
 #pragma unroll
             for (int a = 0; a + 1 < kAhead; ++a) eq[a] = eq[a + 1];
             {
                 const int ta = t + kAhead;
                 eq[kAhead - 1] = (ta < n && l > ta && l < n) ? Ep[w.eidx(l, ta)] : 0.0;
             }
-            const double xt = gbcast<P>(acc * sq_id, t);
+            const double xt = gbcast<P>(kPre ? acc : acc * sq_id, t);
             if (l == t) x = xt;
             acc -= et * xt;
             if (nc >= 0) {
-                const double zt = gbcast<P>(acz * sq_id, t);
+                const double zt = gbcast<P>(kPre ? acz : acz * sq_id, t);
                 if (l == t) zz = zt;
                 acz -= et * zt;
             }
             if (kCollision && nc2 >= 0) {
-                const double zt2 = gbcast<P>(acz2 * sq_id, t);
+                const double zt2 = gbcast<P>(kPre ? acz2 : acz2 * sq_id, t);
                 if (l == t) zz2 = zt2;
                 acz2 -= et * zt2;
             }
             if (kColl3 && nc3 >= 0) {
-                const double zt3 = gbcast<P>(acz3 * sq_id, t);
+                const double zt3 = gbcast<P>(kPre ? acz3 : acz3 * sq_id, t);
                 if (l == t) zz3 = zt3;
                 acz3 -= et * zt3;
             }
@@ -4036,6 +4044,8 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 const int ua = n - 1 - a;
                 bq[a] = (ua >= 0 && l < ua) ? w.Ep()[w.eidx(ua, l)] : 0.0;
             }
+            constexpr bool kPreB = NTM_SUB_PRESCALE && W::kNN > 32;   // as the forward substitution
+            if constexpr (kPreB) { acc *= sq_id; acb *= sq_id; acb2 *= sq_id; }
             for (int u = n - 1; u >= 0; --u) {
                 double eu;
                 if constexpr (kAheadB > 0) {
@@ -4047,16 +4057,17 @@ __device__ __forceinline__ bool polish_compact(const Prob& pb, const W& w, const
                 } else {
                     eu = (l < u) ? w.Ep()[w.eidx(u, l)] : 0.0;
                 }
-                const double mu_u = gbcast<P>(acc * sq_id, u);
+                if constexpr (kPreB) eu *= sq_id;
+                const double mu_u = gbcast<P>(kPreB ? acc : acc * sq_id, u);
                 if (l == u) mu = mu_u;
                 acc -= eu * mu_u;
                 if (kCollision && xb >= 0) {
-                    const double mb_u = gbcast<P>(acb * sq_id, u);
+                    const double mb_u = gbcast<P>(kPreB ? acb : acb * sq_id, u);
                     if (l == u) mb = mb_u;
                     acb -= eu * mb_u;
                 }
                 if (kColl2 && xb2 >= 0) {
-                    const double mb2_u = gbcast<P>(acb2 * sq_id, u);
+                    const double mb2_u = gbcast<P>(kPreB ? acb2 : acb2 * sq_id, u);
                     if (l == u) mb2 = mb2_u;
                     acb2 -= eu * mb2_u;
                 }
